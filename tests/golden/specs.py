@@ -1,0 +1,204 @@
+"""Workload specs shared by the golden generator, the oracle tests and the GPU parity tests.
+
+A spec is a plain dict (JSON-able):
+
+    n, f, mode ('brb' | 'consensus'), nv (key variants per origin), seed, delay_model
+    (0 const, 1 uniform, 2 slow-set, 3 geometric), dmax, dconst, g (global instance id),
+    byzantine (replica ids that run no code), values (value id -> string, id 0 == "-1"),
+    round_cap, step_cap, actions.
+
+actions (each performed after step ``t`` is processed, messages stamped ``t``):
+    {"kind": "propose",  "t", "node", "value"}                 ByzantineRandomizedConsensus.start()
+    {"kind": "brb_send", "t", "node", "kp", "s", "payload"}     BRBroadcast.broadcast(SEND, payload)
+    {"kind": "byz_key",  "t", "kp", "s", "value"[, "payload"]}   declare a Byzantine key
+    {"kind": "byz",      "t", "src", "type", "kp", "s", "dst"}   raw Byzantine message(s)
+"""
+import copy
+
+VALUES = ["-1", "0", "1", "3"]
+SEND, ECHO, READY = 1, 2, 3
+
+
+def _sched(n, f, seed, model, dmax, dconst=1):
+    from oracle.schedule import Schedule
+    return Schedule(n, f, seed, model, dmax, dconst)
+
+
+def brb_spec(n, f, seed, model, dmax, g, sends, dconst=1, byzantine=(), extra=(), step_cap=10000):
+    """sends: list of (t, origin, seq)."""
+    acts = [dict(t=t, kind="brb_send", node=o, kp=o, s=q, payload="TEST %d.%d" % (o + 1, q))
+            for (t, o, q) in sends]
+    acts += list(extra)
+    return dict(n=n, f=f, mode="brb", nv=1, seed=seed, delay_model=model, dmax=dmax, dconst=dconst,
+                g=g, byzantine=list(byzantine), values=VALUES, round_cap=0, step_cap=step_cap,
+                actions=acts)
+
+
+def cons_spec(n, f, seed, model, dmax, g, round_cap=2, proposals=None, byzantine=(), nv=1,
+              starts=None, dconst=1, extra=(), step_cap=4000):
+    """proposals: None -> Philox Bernoulli(1/2) value ids; or a list of value ids.
+    starts: None -> every honest replica proposes at t=0; or a list of start times."""
+    sch = _sched(n, f, seed, model, dmax, dconst)
+    acts = []
+    for i in range(n):
+        if i in byzantine:
+            continue
+        v = sch.proposal_id(g, i) if proposals is None else proposals[i]
+        acts.append(dict(t=0 if starts is None else starts[i], kind="propose", node=i, value=v))
+    acts += list(extra)
+    return dict(n=n, f=f, mode="consensus", nv=nv, seed=seed, delay_model=model, dmax=dmax,
+                dconst=dconst, g=g, byzantine=list(byzantine), values=VALUES, round_cap=round_cap,
+                step_cap=step_cap, actions=acts)
+
+
+def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
+    """SURVEY §8(d) cfg3 pattern: each Byzantine replica b SENDs value "0" to even
+    destinations and "1" to odd ones, then ECHOes and READYs both keys to everyone."""
+    even = sum(1 << d for d in range(0, n, 2))
+    odd = sum(1 << d for d in range(1, n, 2))
+    allm = (1 << n) - 1
+    acts = []
+    for b in byzantine:
+        for v in range(2):
+            acts.append(dict(t=t_send, kind="byz_key", kp=b * nv + v, s=0, value=1 + v))
+        acts.append(dict(t=t_send, kind="byz", src=b, type=SEND, kp=b * nv, s=0, dst=even))
+        acts.append(dict(t=t_send, kind="byz", src=b, type=SEND, kp=b * nv + 1, s=0, dst=odd))
+        for v in range(2):
+            acts.append(dict(t=t_er, kind="byz", src=b, type=ECHO, kp=b * nv + v, s=0, dst=allm))
+            acts.append(dict(t=t_er, kind="byz", src=b, type=READY, kp=b * nv + v, s=0, dst=allm))
+    return acts
+
+
+def _kat(n, f, seq, byz_nodes, key=(1, 0), name=""):
+    """Known-answer scenario: scripted Byzantine peers feed one honest node (node 0)
+    the message sequence `seq` = [(t, type, src[, dst_mask])...] for one BRB key."""
+    allm = (1 << n) - 1
+    kp, s = key
+    acts = [dict(t=0, kind="byz_key", kp=kp, s=s, value=0, payload="KAT %s" % name)]
+    for item in seq:
+        t, typ, src = item[:3]
+        dst = item[3] if len(item) > 3 else allm
+        acts.append(dict(t=t, kind="byz", src=src, type=typ, kp=kp, s=s, dst=dst))
+    return dict(n=n, f=f, mode="brb", nv=1, seed=0, delay_model=0, dmax=1, dconst=1, g=0,
+                byzantine=list(byz_nodes), values=VALUES, round_cap=0, step_cap=200, actions=acts)
+
+
+def kat_specs():
+    """SURVEY §4 K1-K7, K12 restated as scripted scenarios (node 0 honest, delay 1)."""
+    S, E, R = SEND, ECHO, READY
+    k = {}
+    # K1: S, E1, E2, E3, R1, R2, R3 one per step
+    k["K1"] = _kat(4, 1, [(0, S, 1, 1), (1, E, 1), (2, E, 2), (3, E, 3), (4, R, 1), (5, R, 2), (6, R, 3)],
+                   [1, 2, 3], name="K1")
+    # K2: ECHO before SEND: the SEND is then ignored (no ECHO from node 0)
+    k["K2"] = _kat(4, 1, [(0, E, 1), (1, S, 1, 1), (2, E, 2), (3, E, 3), (4, R, 1), (5, R, 2), (6, R, 3)],
+                   [1, 2, 3], name="K2")
+    # K3: READY before the echo quorum blocks node 0's own READY
+    k["K3"] = _kat(4, 1, [(0, S, 1, 1), (1, R, 1), (2, E, 1), (3, E, 2), (4, E, 3), (5, R, 2), (6, R, 3)],
+                   [1, 2, 3], name="K3")
+    # K4 (n=7, f=2): READYs only -> amplification, then delivery
+    k["K4"] = _kat(7, 2, [(0, R, 1), (1, R, 2), (2, R, 3), (3, R, 4), (4, R, 5), (5, R, 6)],
+                   [1, 2, 3, 4, 5, 6], name="K4")
+    # K5: duplicate ECHOs from one sender change nothing (dropped by the network)
+    k["K5"] = _kat(4, 1, [(0, S, 1, 1), (1, E, 1), (2, E, 1), (3, E, 1), (4, E, 2)], [1, 2, 3], name="K5")
+    # K7: after DELIVER everything is ignored
+    k["K7"] = _kat(4, 1, [(0, S, 1, 1), (1, E, 1), (1, E, 2), (1, E, 3), (2, R, 1), (2, R, 2), (2, R, 3),
+                          (5, S, 2), (6, E, 2)], [1, 2, 3], name="K7")
+    # K12 (n=7, f=2): three READYs then silence: node 0 amplifies; its own READY returns
+    k["K12"] = _kat(7, 2, [(0, R, 1), (1, R, 2), (2, R, 3)], [1, 2, 3, 4, 5, 6], name="K12")
+    # same-step mix: S, E and R for one key arriving together
+    k["MIX"] = _kat(4, 1, [(0, S, 1), (0, E, 1), (0, E, 2), (0, E, 3), (1, R, 1), (1, R, 2), (1, R, 3)],
+                    [1, 2, 3], name="MIX")
+    # K6: two payloads from one origin are two independent keys (equivocation undetected)
+    k6 = _kat(4, 1, [(0, S, 1, 1), (1, E, 2), (2, E, 3)], [1, 2, 3], key=(1, 0), name="K6a")
+    k6["actions"] += [dict(t=0, kind="byz_key", kp=1, s=1, value=0, payload="KAT K6b"),
+                      dict(t=0, kind="byz", src=1, type=SEND, kp=1, s=1, dst=1),
+                      dict(t=1, kind="byz", src=2, type=ECHO, kp=1, s=1, dst=15),
+                      dict(t=2, kind="byz", src=3, type=ECHO, kp=1, s=1, dst=15)]
+    k["K6"] = k6
+    for name, sp in k.items():
+        sp["name"] = name
+    return k
+
+
+def cons_kat_specs():
+    """K8-K11: consensus windows fed by scripted (Byzantine-origin) keys."""
+    out = {}
+    n, f = 6, 1
+    allm = (1 << n) - 1
+
+    def deliver_key(acts, b, variant, s, value, t, nv):
+        # a key that every node delivers: Byzantine origin b, SEND + ECHO + READY from the
+        # Byzantine coalition (nodes 2..5), enough to pass every threshold.
+        kp = b * nv + variant
+        acts.append(dict(t=t, kind="byz_key", kp=kp, s=s, value=value))
+        acts.append(dict(t=t, kind="byz", src=b, type=SEND, kp=kp, s=s, dst=allm))
+        for src in (2, 3, 4, 5):
+            acts.append(dict(t=t, kind="byz", src=src, type=ECHO, kp=kp, s=s, dst=allm))
+        for src in (2, 3, 4, 5):
+            acts.append(dict(t=t + 1, kind="byz", src=src, type=READY, kp=kp, s=s, dst=allm))
+
+    # K10: six deliveries all claiming host 2 -> value_count counts deliveries, hosts dedup
+    acts = []
+    for j in range(6):
+        deliver_key(acts, 2, j % 2, j, 1 + (j % 2), 0, 2)
+    sp = cons_spec(n, f, 0, 0, 1, 0, round_cap=1, proposals=[1, 1, 1, 1, 1, 1], byzantine=[2, 3, 4, 5],
+                   nv=2, extra=acts, step_cap=60)
+    sp["name"] = "K10"
+    out["K10"] = sp
+    # K11: round 99 / phase 2 keys count in the current window (round/phase fields ignored)
+    acts = []
+    for j, b in enumerate((2, 3, 4, 5)):
+        deliver_key(acts, b, 0, 2 * 98 + 1, 2, 0, 1)
+    sp = cons_spec(n, f, 0, 0, 1, 0, round_cap=1, proposals=[1, 1, 1, 1, 1, 1], byzantine=[2, 3, 4, 5],
+                   nv=1, extra=acts, step_cap=60)
+    sp["name"] = "K11"
+    out["K11"] = sp
+    return out
+
+
+def scenario_groups():
+    """name -> list of specs.  Sizes chosen so the reference harness finishes in seconds."""
+    G = {}
+    allsends4 = [(0, i, 0) for i in range(4)]
+    G["brb_fifo_n4"] = [brb_spec(4, 1, 1, 0, 1, 0, allsends4)]
+    G["brb_uniform_n4"] = [brb_spec(4, 1, 0x5EED0002, 1, 4, g, allsends4) for g in range(30)]
+    G["brb_geometric_n7"] = [brb_spec(7, 2, 77, 3, 6, g, [(0, i, 0) for i in range(7)]) for g in range(8)]
+    G["brb_uniform_n10"] = [brb_spec(10, 3, 1010, 1, 3, g, [(0, i, 0) for i in range(10)]) for g in range(6)]
+    G["brb_slowset_n16"] = [brb_spec(16, 5, 0x5EED0004, 2, 8, g, [(0, i, 0) for i in range(16)])
+                            for g in range(3)]
+    G["brb_staggered_n5"] = [brb_spec(5, 1, 55, 1, 3, g, [(0, 0, 0), (2, 1, 0), (2, 0, 1), (7, 3, 0), (9, 4, 0),
+                                                         (9, 0, 2), (30, 2, 0)]) for g in range(8)]
+    G["brb_byz_n7"] = [brb_spec(7, 2, 99, 1, 4, g, [(0, i, 0) for i in range(5)], byzantine=[5, 6],
+                                extra=[dict(t=0, kind="byz_key", kp=5, s=0, value=0, payload="BYZ 5"),
+                                       dict(t=0, kind="byz", src=5, type=SEND, kp=5, s=0, dst=0b0010101),
+                                       dict(t=1, kind="byz", src=5, type=ECHO, kp=5, s=0, dst=127),
+                                       dict(t=1, kind="byz", src=6, type=ECHO, kp=5, s=0, dst=127),
+                                       dict(t=2, kind="byz", src=6, type=READY, kp=5, s=0, dst=127),
+                                       dict(t=1, kind="byz", src=6, type=READY, kp=0, s=0, dst=127)])
+                       for g in range(8)]
+    G["kat"] = list(kat_specs().values()) + list(cons_kat_specs().values())
+    G["cons_brc_test_n6"] = [cons_spec(6, 1, 3, 0, 1, 0, round_cap=3, proposals=[3] * 6)]
+    G["cons_staggered_n6"] = [cons_spec(6, 1, 6, 1, 3, g, round_cap=2, proposals=[3] * 6,
+                                        starts=[0, 5, 5, 12, 20, 21]) for g in range(4)]
+    G["cons_uniform_n4"] = [cons_spec(4, 1, 0x5EED0002, 1, 4, g, round_cap=2) for g in range(20)]
+    G["cons_const_n6"] = [cons_spec(6, 1, 16, 0, 1, g, round_cap=3) for g in range(6)]
+    G["cons_uniform_n6"] = [cons_spec(6, 1, 61, 1, 4, g, round_cap=2) for g in range(16)]
+    G["cons_slowset_n7"] = [cons_spec(7, 2, 71, 2, 4, g, round_cap=3) for g in range(8)]
+    G["cons_geometric_n10"] = [cons_spec(10, 3, 103, 3, 5, g, round_cap=2) for g in range(6)]
+    byz16 = list(range(11, 16))
+    G["cons_equivocate_n16"] = [cons_spec(16, 5, 0x5EED0003, m, d, g, round_cap=1, byzantine=byz16, nv=2,
+                                          extra=equivocation_actions(16, byz16))
+                                for (m, d) in ((1, 4), (2, 4), (0, 1)) for g in range(2)]
+    G["cons_slowset_n16"] = [cons_spec(16, 5, 0x5EED0004, 2, 8, g, round_cap=2) for g in range(3)]
+    G["cons_slowset_n64"] = [cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1) for g in range(1)]
+    for name, specs in G.items():
+        for i, sp in enumerate(specs):
+            sp.setdefault("name", "%s/%d" % (name, i))
+    return G
+
+
+def clone(spec, **kw):
+    sp = copy.deepcopy(spec)
+    sp.update(kw)
+    return sp

@@ -1,0 +1,143 @@
+/*
+ * brc.h -- C-ABI of the MI355X batched consensus engine (libbrc_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path.  The reference exposes it as Python
+ * classes; this ABI is what those classes (re-implemented in
+ * byzantinerandomizedconsensus_amd/) bind through ctypes:
+ *
+ *   reference                                                   replaced by
+ *   ---------------------------------------------------------   ----------------------------
+ *   BRBroadcast.__init__ / ByzantineRandomizedConsensus.__init__ brc_create
+ *     (core/brbroadcast.py:17-44, core/byzantinerandomizedconsensus.py:18-36)
+ *   BRBroadcast.broadcast_listener (core/brbroadcast.py:121-128) brc_run (the accept loop,
+ *     + the listener loop body (core/brbroadcast.py:60-119)       batched over instances)
+ *   Broadcast.broadcast(SEND, m)     (base/broadcast.py:17-40)   brc_inject(BRC_INJ_SEND)
+ *   ByzantineRandomizedConsensus.start/propose (:38-51)          brc_inject(BRC_INJ_PROPOSE) /
+ *                                                                brc_load_proposals
+ *   IBroadcastHandler.deliver upcall (base/broadcast.py:52-55)   brc_read_events (DELIVER)
+ *   IConsensusHandler.decide upcall  (base/consensus.py:22-24)   brc_read_events (DECIDE),
+ *                                                                brc_read_replicas
+ *   (Byzantine peers: raw sends into the transport)              brc_inject(BRC_INJ_KEY/SEND/MSG),
+ *                                                                brc_load_byzantine
+ *
+ * Conventions: every call returns 0 on success or a negative BRC_E_* code; host buffers
+ * are caller-owned; device buffers are engine-owned; one host thread per engine; all work
+ * is ordered on the engine's own HIP stream; no callbacks cross the ABI.
+ */
+#ifndef BRC_H
+#define BRC_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BRC_ABI_VERSION 1
+
+enum {
+    BRC_OK = 0,
+    BRC_E_INVALID = -1,      /* bad argument / unsupported configuration */
+    BRC_E_NOMEM = -2,        /* device or host allocation failed */
+    BRC_E_HIP = -3,          /* HIP runtime error (see brc_last_error) */
+    BRC_E_UNSUPPORTED = -4,  /* a workload feature the engine does not model */
+    BRC_E_STATE = -5         /* call not valid in the current engine state */
+};
+
+enum { BRC_PROTO_BRB = 0, BRC_PROTO_CONSENSUS = 1 };
+enum { BRC_PEER_SENDER = 0 };
+enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DELAY_GEOMETRIC = 3 };
+enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };
+enum { BRC_BYZ_NONE = 0, BRC_BYZ_EQUIVOCATE = 1 };
+enum { BRC_SEND = 1, BRC_ECHO = 2, BRC_READY = 3 };
+enum { BRC_INJ_PROPOSE = 1, BRC_INJ_SEND = 2, BRC_INJ_KEY = 3, BRC_INJ_MSG = 4 };
+enum { BRC_RUNNING = 0, BRC_DONE = 1, BRC_QUIESCENT = 2, BRC_STEPCAP = 3, BRC_OVERFLOW = 4, BRC_BADINJ = 5 };
+enum { BRC_EV_DELIVER = 1, BRC_EV_DECIDE = 2, BRC_EV_SEND = 3 };
+
+typedef struct {
+    uint32_t n;               /* replicas per instance, self included (1..64) */
+    uint32_t f;               /* fault bound: thresholds (n+f)/2, f+1, 2f+1, n-f+1 */
+    uint32_t protocol;        /* BRC_PROTO_* */
+    uint32_t peer_mode;       /* BRC_PEER_SENDER (core/brbroadcast.py:71 identity) */
+    uint64_t instances;       /* instances owned by this engine */
+    uint64_t instance_offset; /* global id of instance 0 (Philox counter; multi-GPU shard) */
+    uint64_t seed;            /* schedule seed (delays, proposals, slow set) */
+    uint32_t delay_model;     /* BRC_DELAY_* */
+    uint32_t delay_max;       /* D, 1..16 */
+    uint32_t delay_const;     /* BRC_DELAY_CONST value */
+    uint32_t round_cap;       /* consensus: instance DONE when every honest replica decided this many times */
+    uint32_t step_cap;        /* last simulated step (<= 60000) */
+    uint32_t key_window;      /* Q: live phase indices per origin (2, 4 or 8) */
+    uint32_t variants;        /* NV: key variants per origin (1, 2 or 4; Q*NV <= 8) */
+    uint32_t proposals;       /* BRC_PROPOSALS_* (consensus) */
+    uint32_t byz_pattern;     /* BRC_BYZ_* applied to every instance */
+    uint32_t event_capacity;  /* 0: no event log */
+    uint64_t byzantine_mask;  /* replicas that run no code (all instances; see brc_load_byzantine) */
+    int32_t device;           /* HIP device ordinal */
+    uint32_t reserved[7];
+} brc_config;
+
+typedef struct {
+    uint32_t t;               /* action time: performed after step t, messages stamped t */
+    uint16_t kind;            /* BRC_INJ_* */
+    uint16_t type;            /* BRC_INJ_MSG: BRC_ECHO / BRC_READY */
+    uint64_t instance;        /* engine-local instance index */
+    uint32_t node;            /* proposer / sender */
+    uint32_t kp;              /* key slot: origin * variants + variant */
+    uint32_t s;               /* phase index 2*(round-1)+(phase-1), or BRB sequence */
+    int32_t value;            /* value id (0 == "-1") */
+    uint64_t dst_mask;        /* BRC_INJ_SEND destinations; BRC_INJ_MSG must be all peers */
+} brc_injection;
+
+typedef struct {
+    uint32_t status;          /* BRC_RUNNING ... */
+    uint32_t t_stop;          /* last step with an arrival at an honest replica or an action */
+    uint32_t t_now;           /* engine time of the instance's wave */
+    uint32_t decided;         /* every honest replica decided at least once */
+    uint64_t msgs_sent;       /* link messages sent (duplicate-suppressed) */
+    uint64_t arrivals;        /* messages processed by honest replicas (replica-message-steps) */
+    uint64_t cell_steps;      /* (receiver, key) cells that had arrivals, summed over steps */
+    uint64_t deliveries;
+} brc_instance_result;
+
+typedef struct {
+    uint32_t round, phase, value_count, decide_count;
+    uint32_t first_decide_round, first_decide_t;
+    int32_t first_decide_value, last_decide_value;
+} brc_replica_result;
+
+typedef struct {
+    uint64_t instance;
+    uint32_t t;
+    uint8_t kind, node, type, pad;
+    uint32_t a, b;            /* DELIVER: kp, s   DECIDE: round, value   SEND: kp, s */
+} brc_event;
+
+typedef struct {
+    uint64_t instances, running, done, quiescent, stepcap, overflow, decided;
+    uint64_t msgs_sent, arrivals, cell_steps, deliveries;
+    uint64_t decide_rounds_sum;   /* sum of first-decide rounds over honest replicas */
+    uint64_t max_t;
+    uint64_t events_dropped;
+} brc_stats;
+
+int brc_create(const brc_config* cfg, void** engine);
+int brc_load_proposals(void* engine, const int8_t* proposals /* [instances][n] value ids */);
+int brc_load_byzantine(void* engine, const uint64_t* byz_masks /* [instances] */);
+int brc_inject(void* engine, const brc_injection* list, size_t count);
+int brc_run(void* engine, uint32_t max_steps, uint32_t* running_left);
+int brc_reset(void* engine);
+int brc_read_instances(void* engine, uint64_t first, uint64_t count, brc_instance_result* out);
+int brc_read_replicas(void* engine, uint64_t first, uint64_t count, brc_replica_result* out /* [count][n] */);
+int brc_read_events(void* engine, brc_event* out, size_t cap, size_t* count);
+int brc_read_stats(void* engine, brc_stats* out);
+int brc_last_kernel_ms(void* engine, float* ms);
+int brc_device_count(int* count);
+const char* brc_last_error(void* engine);
+void brc_destroy(void* engine);
+int brc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -35,7 +35,18 @@ def digest(rows):
     return hashlib.sha256(json.dumps(rows, separators=(",", ":")).encode()).hexdigest()
 
 
+def canonical(result):
+    """Event lists in canonical sorted order (the engine reports events per step, not in the
+    reference's processing order; within a (step, node) both orders are (kp, s))."""
+    ev = result["events"]
+    key = lambda r: [str(x) if isinstance(x, str) else x for x in r]  # noqa: E731
+    out = dict(result)
+    out["events"] = {k: sorted(map(list, ev[k]), key=key) for k in ("deliver", "decide", "send")}
+    return out
+
+
 def compact(result):
+    result = canonical(result)
     ev = result["events"]
     out = {k: result[k] for k in ("status", "t_stop", "msgs_sent", "arrivals")}
     out["counts"] = {k: len(v) for k, v in ev.items()}

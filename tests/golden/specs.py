@@ -101,9 +101,11 @@ def kat_specs():
                    [1, 2, 3, 4, 5, 6], name="K4")
     # K5: duplicate ECHOs from one sender change nothing (dropped by the network)
     k["K5"] = _kat(4, 1, [(0, S, 1, 1), (1, E, 1), (2, E, 1), (3, E, 1), (4, E, 2)], [1, 2, 3], name="K5")
-    # K7: after DELIVER everything is ignored
-    k["K7"] = _kat(4, 1, [(0, S, 1, 1), (1, E, 1), (1, E, 2), (1, E, 3), (2, R, 1), (2, R, 2), (2, R, 3),
-                          (5, S, 2), (6, E, 2)], [1, 2, 3], name="K7")
+    # K7: after DELIVER everything is ignored (fresh ECHO/READY from node 4 arrive afterwards).
+    # (A second SEND of one key from another sender is not modelled by the engine: brc_inject
+    # rejects it with BRC_E_UNSUPPORTED; honest nodes never send it.)
+    k["K7"] = _kat(5, 1, [(0, S, 1, 1), (1, E, 1), (1, E, 2), (1, E, 3), (2, R, 1), (2, R, 2), (2, R, 3),
+                          (5, E, 4), (6, R, 4)], [1, 2, 3, 4], name="K7")
     # K12 (n=7, f=2): three READYs then silence: node 0 amplifies; its own READY returns
     k["K12"] = _kat(7, 2, [(0, R, 1), (1, R, 2), (2, R, 3)], [1, 2, 3, 4, 5, 6], name="K12")
     # same-step mix: S, E and R for one key arriving together

@@ -1,0 +1,39 @@
+"""Loading and comparing the golden fixtures (tests/golden/*.json)."""
+import glob
+import hashlib
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def groups():
+    out = {}
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "*.json"))):
+        with open(path) as fh:
+            data = json.load(fh)
+        out[data["group"]] = data["cases"]
+    return out
+
+
+def digest(rows):
+    return hashlib.sha256(json.dumps(rows, separators=(",", ":")).encode()).hexdigest()
+
+
+def canonical_events(ev):
+    key = lambda r: [str(x) if isinstance(x, str) else x for x in r]  # noqa: E731
+    return {k: sorted(map(list, ev[k]), key=key) for k in ("deliver", "decide", "send")}
+
+
+def assert_matches(expected, got, label=""):
+    """expected: fixture 'result' (compact form); got: result with canonical event lists."""
+    for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        assert got[k] == expected[k], "%s: %s differs: got %r expected %r" % (label, k, got[k], expected[k])
+    ev = canonical_events(got["events"])
+    for k in ("deliver", "decide", "send"):
+        assert len(ev[k]) == expected["counts"][k], "%s: %d %s events, expected %d" % (
+            label, len(ev[k]), k, expected["counts"][k])
+        if k in expected["events"]:
+            assert ev[k] == expected["events"][k], "%s: %s events differ" % (label, k)
+        assert digest(ev[k]) == expected["digest"][k], "%s: %s digest differs" % (label, k)

@@ -1,0 +1,95 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the reference's golden fixtures and
+against the C oracle on fresh seeded workloads.  Bar: bit-exact (status, last active step,
+message counts and every ordered delivery / decide / send event)."""
+import random
+
+import pytest
+
+from oracle import oracle
+from tests import golden_io
+from tests.golden import specs as S
+
+pytestmark = pytest.mark.gpu
+
+GROUPS = golden_io.groups()
+
+
+@pytest.fixture(scope="module")
+def runner():
+    from tests import engine_runner
+    return engine_runner
+
+
+@pytest.mark.parametrize("group", sorted(GROUPS))
+def test_engine_matches_reference_fixtures(runner, group):
+    cases = GROUPS[group]
+    got = runner.run_specs([c["spec"] for c in cases])
+    for i, (c, r) in enumerate(zip(cases, got)):
+        golden_io.assert_matches(c["result"], r, "%s[%d]" % (group, i))
+
+
+def _compare_with_oracle(runner, specs):
+    got = runner.run_specs(specs)
+    for sp, r in zip(specs, got):
+        exp = oracle.run(sp)
+        exp["events"] = golden_io.canonical_events(exp["events"])
+        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+            assert r[k] == exp[k], "%s %s: %r vs oracle %r" % (sp["name"], k, r[k], exp[k])
+        for k in ("deliver", "decide", "send"):
+            assert r["events"][k] == exp["events"][k], "%s: %s events differ" % (sp["name"], k)
+    return got
+
+
+@pytest.mark.parametrize("n,f,model,dmax", [(4, 1, 1, 4), (7, 2, 3, 6), (16, 5, 1, 4), (13, 4, 2, 5)])
+def test_brb_random_vs_oracle(runner, n, f, model, dmax):
+    rng = random.Random(n * 1000 + dmax)
+    specs = []
+    for g in range(48):
+        sends = [(rng.randint(0, 5), o, q) for o in range(n) for q in range(rng.randint(0, 2))]
+        sp = S.brb_spec(n, f, 0xBEEF + n, model, dmax, 1000 + g, sends)
+        sp["name"] = "brb%d/%d" % (n, g)
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+@pytest.mark.parametrize("n,f,model,dmax,rcap", [(4, 1, 1, 4, 3), (6, 1, 1, 3, 2), (7, 2, 2, 4, 3),
+                                                  (10, 3, 3, 5, 2), (16, 5, 2, 8, 2), (16, 3, 1, 2, 2),
+                                                  (31, 10, 2, 6, 1), (33, 10, 1, 3, 1)])
+def test_consensus_random_vs_oracle(runner, n, f, model, dmax, rcap):
+    specs = []
+    for g in range(32):
+        sp = S.cons_spec(n, f, 0xC0DE + n, model, dmax, 500 + g, round_cap=rcap)
+        sp["name"] = "cons%d/%d" % (n, g)
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+def test_consensus_n64_slowset_vs_oracle(runner):
+    specs = []
+    for g in range(6):
+        sp = S.cons_spec(64, 21, 0x5EED0004, 2, 8, 77 + g, round_cap=1)
+        sp["name"] = "cfg4/%d" % g
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+def test_equivocation_vs_oracle(runner):
+    byz = list(range(11, 16))
+    specs = []
+    for g in range(16):
+        sp = S.cons_spec(16, 5, 0x5EED0003, 1, 4, 3000 + g, round_cap=1, byzantine=byz, nv=2,
+                         extra=S.equivocation_actions(16, byz))
+        sp["name"] = "cfg3/%d" % g
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+def test_staggered_starts_vs_oracle(runner):
+    rng = random.Random(5)
+    specs = []
+    for g in range(24):
+        sp = S.cons_spec(6, 1, 99, 1, 3, 9000 + g, round_cap=2,
+                         starts=[rng.choice([0, 0, rng.randint(1, 12)]) for _ in range(6)])
+        sp["name"] = "stag/%d" % g
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)

@@ -1,0 +1,176 @@
+#!/usr/bin/env python3
+"""Headline benchmark: decided consensus instances/sec at n=64, f=21 (BASELINE.json configs[3]).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--instances I]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (multi-GPU)
+
+Workload: 64 replicas, f = 21, the reference's protocol exactly as it
+runs (Bracha broadcast + two-phase consensus, reference quirks included), adversarial delays
+(messages from/to a per-instance slow set of f replicas take D = 8 steps, all others 1),
+Philox Bernoulli(1/2) proposals.  One "step" = one full pass of the hot path over the batch:
+every instance simulated from its proposals until every honest replica has decided (the
+reference's decide() upcall, core/byzantinerandomizedconsensus.py:94).  Instances are
+independent, so ranks shard them (global Philox ids => results independent of N: weak
+scaling); the only collective is one RCCL all-reduce of the statistics.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_REPLICAS, F_FAULTS, DELAY_MAX, SEED = 64, 21, 8, 0x5EED0004
+SURVEY_BYTES_PER_CELL_STEP = 6 * ((N_REPLICAS + 7) // 8) + 2   # 50 B at n=64
+HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--instances", type=int, default=1 << 17, help="instances per GPU")
+    ap.add_argument("--key-window", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """The C oracle (a scalar port of the reference's path, 1 core) on the same workload:
+    the first instances of the batch, until `seconds` of CPU work have been spent."""
+    from oracle import oracle
+    from tests.golden import specs as S
+    t0 = time.perf_counter()
+    done = arrivals = count = 0
+    while time.perf_counter() - t0 < seconds:
+        sp = S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, count, round_cap=1)
+        r = oracle.run(sp)
+        done += r["status"] == "done"
+        arrivals += r["arrivals"]
+        count += 1
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "decided instances/s", "cores": 1, "kind": "port",
+            "sample": "%d instances of the same workload (global ids 0..%d), %.1f s, C oracle "
+                      "(oracle/brc_oracle.c, event-by-event restatement); %.3g replica-message-steps/s"
+                      % (count, count - 1, dt, arrivals / dt)}
+
+
+def load_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        return d
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl")
+        dist = tdist
+
+    from byzantinerandomizedconsensus_amd import _lib as L
+    from byzantinerandomizedconsensus_amd.engine import Engine
+
+    per = args.instances
+    eng = Engine(n=N_REPLICAS, f=F_FAULTS, instances=per, protocol="consensus", seed=SEED,
+                 delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=1, step_cap=4000,
+                 key_window=args.key_window, variants=1, proposals=L.PROPOSALS_PHILOX,
+                 instance_offset=rank * per, device=local)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def one_step():
+        eng.reset()
+        eng.run()
+        return eng.last_kernel_ms()
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        kms.append(one_step())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.stats()
+    local_stats = [st["decided"], st["done"], st["overflow"] + st["stepcap"] + st["running"],
+                   st["arrivals"], st["cell_steps"], st["msgs_sent"]]
+    kernel_ms = sum(kms) / len(kms)
+    if dist is not None:
+        import torch
+        t = torch.tensor(local_stats, dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)                                   # RCCL over xGMI: statistics only
+        local_stats = [int(x) for x in t.tolist()]
+        m = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = m.tolist()
+    decided, done, bad, arrivals, cell_steps, msgs = local_stats
+    if bad:
+        print("WARNING: %d instances did not finish cleanly" % bad, file=sys.stderr)
+    value = decided * args.steps / elapsed
+    out = None
+    if rank == 0:
+        achieved = SURVEY_BYTES_PER_CELL_STEP * (cell_steps / world) / (kernel_ms / 1e3) / 1e9
+        tr = load_traffic()
+        traffic = None
+        if tr and tr.get("instances") == per and tr.get("workload") == "cfg4":
+            traffic = tr.get("hbm_bytes_per_launch")
+        out = {
+            "metric": "decided consensus instances/sec (node) at n=64,f=21",
+            "value": value,
+            "unit": "instances/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
+            "config": {"workload": "cfg4: n=64 f=21 reference-protocol consensus to first decision, "
+                                   "slow-set delays D=8, %d instances/GPU" % per,
+                       "n": N_REPLICAS, "f": F_FAULTS, "instances_per_gpu": per, "round_cap": 1,
+                       "key_window": args.key_window, "parallelism": "instance-sharded x%d" % world},
+            "replica_message_steps_per_s": arrivals * args.steps / world * world / elapsed,
+            "decided_fraction": decided / float(per * world),
+            "kernel_ms": kernel_ms,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "note": "algorithmic = %d B (SURVEY 8(d)) x %d cell-steps per launch per GPU"
+                                 % (SURVEY_BYTES_PER_CELL_STEP, cell_steps // world)},
+        }
+    eng.close()
+    if rank == 0 and not args.no_cpu and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
 ABI_VERSION = 1
 
@@ -87,7 +87,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(name, ctypes.c_uint64) for name in (
         "instances", "running", "done", "quiescent", "stepcap", "overflow", "decided",
         "msgs_sent", "arrivals", "cell_steps", "deliveries", "decide_rounds_sum", "max_t",
-        "events_dropped")]
+        "events_dropped", "lane_loads")]
 
 
 _lib = None

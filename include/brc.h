@@ -119,6 +119,7 @@ typedef struct {
     uint64_t decide_rounds_sum;   /* sum of first-decide rounds over honest replicas */
     uint64_t max_t;
     uint64_t events_dropped;
+    uint64_t lane_loads;          /* cell words read (one per real lane per processed key-step) */
 } brc_stats;
 
 int brc_create(const brc_config* cfg, void** engine);

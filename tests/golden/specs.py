@@ -143,7 +143,7 @@ def cons_kat_specs():
     # K10: six deliveries all claiming host 2 -> value_count counts deliveries, hosts dedup
     acts = []
     for j in range(6):
-        deliver_key(acts, 2, j % 2, j, 1 + (j % 2), 0, 2)
+        deliver_key(acts, 2, j % 2, j // 2, 1 + (j % 2), 0, 2)
     sp = cons_spec(n, f, 0, 0, 1, 0, round_cap=1, proposals=[1, 1, 1, 1, 1, 1], byzantine=[2, 3, 4, 5],
                    nv=2, extra=acts, step_cap=60)
     sp["name"] = "K10"

@@ -43,7 +43,7 @@ namespace {
 constexpr int TS = 32;            // activity ring (steps); > max delay
 constexpr int WPB = 4;            // independent waves per workgroup
 #ifndef BRC_CHUNK
-#define BRC_CHUNK 4
+#define BRC_CHUNK 8
 #endif
 constexpr int CHUNK = BRC_CHUNK;  // key slots processed together (memory-level parallelism)
 constexpr uint32_t NEVER = 0xFFFFu;
@@ -113,6 +113,18 @@ template <int NPAD, typename T> __device__ __forceinline__ T seg_or(T x) {
 }
 
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return x ? 32u - (uint32_t)__clz(x) : 0u; }
+
+// compile-time unrolled loop: f(IC<0>{}), ..., f(IC<N-1>{}) (register arrays stay statically indexed)
+template <int I> struct IC { static constexpr int value = I; };
+template <int N> struct Unrolled {
+    template <typename F> __device__ __forceinline__ static void run(F&& f) {
+        Unrolled<N - 1>::run(f);
+        f(IC<N - 1>{});
+    }
+};
+template <> struct Unrolled<0> {
+    template <typename F> __device__ __forceinline__ static void run(F&&) {}
+};
 
 // wave-uniform value -> scalar registers (valid only when every lane holds the same value)
 __device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
@@ -185,14 +197,16 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
     if (item >= P.nitems) return;               // whole wave exits; waves never synchronise
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
     // per-wave LDS carve: meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 |
-    //                     L[DM][64] T | mgen[IPW*NK] u32 | any u32
+    //                     L[DM][64] T | hm[4][64] T | mgen[IPW*NK] u32 | any u32
     const uint32_t l_words = (DM * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    const uint32_t per_wave_words = IPW * NK + TS * nkw + 64 * nkw + l_words + (IPW * NK + 2) / 2 + 1;
+    const uint32_t h_words = (4 * 64 * (uint32_t)sizeof(T) + 7) / 8;
+    const uint32_t per_wave_words = IPW * NK + TS * nkw + 64 * nkw + l_words + h_words + (IPW * NK + 2) / 2 + 1;
     uint64_t* s_meta = smem + (size_t)wid * per_wave_words;
     uint64_t* s_act = s_meta + IPW * NK;
     uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
     T* s_L = (T*)(s_dbits + 64 * nkw);           // s_L[i*64 + lane]: senders at delay i+1
-    uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + l_words);
+    T* s_hm = (T*)(s_dbits + 64 * nkw + l_words);   // s_hm[v*64 + lane]: hosts that delivered value v
+    uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + l_words + h_words);
     uint32_t* s_any = s_gen + IPW * NK;
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
@@ -219,9 +233,11 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
         if (lane == 0) *s_any = P.actany[item];
     }
 
-    InstState ist = {BRC_DONE, 0, 0, 0, 0, 0};
-    if (iex) ist = P.inst[inst];
-    uint32_t status = ist.status, t_stop = ist.t_stop, q_until = ist.q_until;
+    uint32_t status = BRC_DONE, t_stop = 0, q_until = 0;
+    if (iex) {
+        const uint64_t w0 = *(const uint64_t*)&P.inst[inst];     // status | t_stop | q_until | flags
+        status = w0 & 0xFFFF; t_stop = (w0 >> 16) & 0xFFFF; q_until = (w0 >> 32) & 0xFFFF;
+    }
     const uint64_t byzm = iex ? P.byz[inst] : ~0ull;
     const bool real = iex && (uint32_t)d < n;
     const bool honest = real && !((byzm >> d) & 1ull);
@@ -269,18 +285,15 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
         s_L[i * 64 + lane] = L[i];
     }
     const uint32_t maxout = hibit(outset);
+    const uint32_t dset = uni32(wave_or(outset));    // every delay some link of this wave has
+    uint64_t* const mycells = P.cells + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
-    T hm0 = 0, hm1 = 0, hm2 = 0, hm3 = 0;
     const size_t li = item * 64 + lane;
-    if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
-        c0 = P.cons0[li]; c1 = P.cons1[li];
-        hm0 = ((const T*)P.hmask)[(item * 4 + 0) * 64 + lane];
-        hm1 = ((const T*)P.hmask)[(item * 4 + 1) * 64 + lane];
-        hm2 = ((const T*)P.hmask)[(item * 4 + 2) * 64 + lane];
-        hm3 = ((const T*)P.hmask)[(item * 4 + 3) * 64 + lane];
-    }
+    const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
+    if (cons_lane) { c0 = P.cons0[li]; c1 = P.cons1[li]; }
+    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? ((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
     uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
     uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
@@ -322,22 +335,23 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
         st_smax = max(st_smax, s);
         log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
     };
-    auto hsel = [&](uint32_t v) -> T { return v == 0 ? hm0 : v == 1 ? hm1 : v == 2 ? hm2 : hm3; };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
             const uint32_t v = (order >> (2 * i)) & 3;
-            if (2 * popc(hsel(v)) > bound2) return v;
+            if (2 * popc(s_hm[v * 64 + lane]) > bound2) return v;
         }
         return 0;                                                    // str(NONE) == "-1"
     };
-    auto cons_reset = [&]() { vcount = 0; nvals = 0; order = 0; hm0 = hm1 = hm2 = hm3 = 0; };
+    auto cons_reset = [&]() {
+        vcount = 0; nvals = 0; order = 0;
+        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
+    };
     auto cons_deliver = [&](uint32_t k) {                            // :53-106
         const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = (k / Q) / NV;
         bool found = false;
         for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
         if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
-        const T hb = (T)((T)1 << host);                              // :60
-        if (v == 0) hm0 |= hb; else if (v == 1) hm1 |= hb; else if (v == 2) hm2 |= hb; else hm3 |= hb;
+        s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
         ++vcount;                                                    // :61
         if (vcount >= P.T_cnt && phase == 1) {                       // :71
             const uint32_t prop = get_max_val(P.bound_p1);           // :73
@@ -480,63 +494,54 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
         bool lane_active = false, any_del = false;
 #pragma unroll 1
         for (uint32_t w = 0; w < nkw; ++w) {
-            uint64_t rem = s_act[row * nkw + w];
+            uint64_t rem = uni64(s_act[row * nkw + w]);
             while (rem) {
                 uint32_t kc[CHUNK];
                 bool vc[CHUNK];
-                uint64_t mc[CHUNK], wc[CHUNK];
-                uint32_t gc[CHUNK];
-                // phase A: metadata from LDS and every lane's cell word from HBM, all issued first
-#pragma unroll
-                for (int c = 0; c < CHUNK; ++c) {
+                uint64_t wc[CHUNK];
+                // phase A: every lane's cell word of CHUNK key slots, all loads in flight at once
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
                     vc[c] = rem != 0;
-                    const uint32_t b = vc[c] ? (uint32_t)(__ffsll((unsigned long long)rem) - 1) : 0u;
+                    kc[c] = w * 64 + (vc[c] ? (uint32_t)(__ffsll((unsigned long long)rem) - 1) : 0u);
                     rem &= rem - 1;
-                    kc[c] = w * 64 + b;
-                    mc[c] = 0; gc[c] = 0; wc[c] = TIMES_NEVER;
-                    if (vc[c]) {
-                        mc[c] = s_meta[mbase + kc[c]];
-                        gc[c] = s_gen[mbase + kc[c]];
-                        if (IPW == 1) { mc[c] = uni64(mc[c]); gc[c] = uni32(gc[c]); }   // one instance per wave
-                        if (running && real && m_s1(mc[c]) != 0)
-                            wc[c] = P.cells[((size_t)item * NK + kc[c]) * 64 + lane];
-                    }
-                }
+                    wc[c] = vc[c] ? mycells[(size_t)kc[c] * 64] : TIMES_NEVER;
+                });
                 // phase B: arrivals (ballots over senders), closed-form update, sends
-#pragma unroll
-                for (int c = 0; c < CHUNK; ++c) {
-                    if (!vc[c]) continue;
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    if (!vc[c]) return;
                     const uint32_t k = kc[c];
-                    const uint64_t m = mc[c];
+                    uint64_t m = s_meta[mbase + k];
+                    uint32_t gw = s_gen[mbase + k];
+                    if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
                     const bool live = running && m_s1(m) != 0;
-                    const uint64_t word = wc[c];
+                    const uint64_t word = (live && real) ? wc[c] : TIMES_NEVER;
                     const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
+                    const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
                     uint32_t ea = 0, ra = 0;
-#pragma unroll
-                    for (int i = 0; i < DM; ++i) {
-                        if ((uint32_t)i < D) {
-                            const uint32_t ts = t - (uint32_t)(i + 1);
-                            const uint64_t be = __ballot(tE == ts), br = __ballot(tR == ts);
-                            if (be | br) {
-                                const T Li = s_L[i * 64 + lane];
-                                ea += popc((T)(be >> segbase) & Li);
-                                ra += popc((T)(br >> segbase) & Li);
-                            }
+                    for (uint32_t ds = dset; ds; ds &= ds - 1) {         // only delays some link has
+                        const uint32_t i = __ffs(ds) - 1;
+                        const uint64_t be = __ballot(dE == i + 1), br = __ballot(dR == i + 1);
+                        if (be | br) {
+                            const T Li = s_L[i * 64 + lane];
+                            ea += popc((T)(be >> segbase) & Li);
+                            ra += popc((T)(br >> segbase) & Li);
                         }
                     }
                     bool s_arr = false;
                     if (live && honest) {
                         const uint32_t dt = t - m_tsend(m);
                         if (dt >= 1 && dt <= D) {
-                            const bool to_me = !(gc[c] & GEN_RESTRICTED) || ((P.kdst[inst * NK + k] >> d) & 1ull);
+                            const bool to_me = !(gw & GEN_RESTRICTED) || ((P.kdst[inst * NK + k] >> d) & 1ull);
                             s_arr = to_me && ((s_L[(dt - 1) * 64 + lane] >> m_sender(m)) & 1);
                         }
                     }
                     const bool has = live && honest && (s_arr || ea || ra);
                     bool echo_send = false, ready_send = false, deliver = false;
-                    if (live && real) st_loads += 1;
+                    st_loads += (live && real) ? 1u : 0u;
                     if (has) {
-                        const uint32_t gen = gc[c] & GEN_MASK;
+                        const uint32_t gen = gw & GEN_MASK;
                         uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
                         uint32_t tEn = tE, tRn = tR;
                         if ((((uint32_t)word >> 19) & GEN_MASK) != gen) { fl = 0; ec = 0; rc = 0; tEn = NEVER; tRn = NEVER; }
@@ -544,18 +549,22 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
                                         echo_send, ready_send, deliver);
                         if (echo_send) tEn = t;
                         if (ready_send) tRn = t;
-                        P.cells[((size_t)item * NK + k) * 64 + lane] =
+                        mycells[(size_t)k * 64] =
                             (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) | ((uint64_t)gen << 19) |
                             ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
                         st_arr += ea + ra + (s_arr ? 1u : 0u);
                         st_cells += 1;
-                        const uint32_t kp = k / Q, s = m_s1(m) - 1u;
-                        if (echo_send) { st_msgs += n; log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s); }
-                        if (ready_send) { st_msgs += n; log_ev(BRC_EV_SEND, d, BRC_READY, kp, s); }
+                        if (echo_send) st_msgs += n;
+                        if (ready_send) st_msgs += n;
                         if (deliver) {
                             st_del += 1; any_del = true;
                             s_dbits[w * 64 + lane] |= 1ull << (k & 63);
-                            log_ev(BRC_EV_DELIVER, d, 0, kp, s);
+                        }
+                        if (P.event_cap) {
+                            const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                            if (echo_send) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
+                            if (ready_send) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
+                            if (deliver) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
                         }
                     }
                     lane_active |= has;
@@ -569,7 +578,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
                             q_until = max(q_until, myq);
                         }
                     }
-                }
+                });
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -650,10 +659,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
                       ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
         P.cons1[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                       ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
-        ((T*)P.hmask)[(item * 4 + 0) * 64 + lane] = hm0;
-        ((T*)P.hmask)[(item * 4 + 1) * 64 + lane] = hm1;
-        ((T*)P.hmask)[(item * 4 + 2) * 64 + lane] = hm2;
-        ((T*)P.hmask)[(item * 4 + 3) * 64 + lane] = hm3;
+        for (int v = 0; v < 4; ++v) ((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
     }
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
@@ -663,9 +669,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) 
         for (int o = NPAD / 2; o; o >>= 1) sums[q] += (uint32_t)__shfl_xor((int)sums[q], o);
     }
     if (iex && d == 0) {
-        InstState o = ist;
-        o.status = (uint16_t)status; o.t_stop = (uint16_t)t_stop; o.q_until = (uint16_t)q_until;
-        P.inst[inst] = o;
+        uint64_t* ip = (uint64_t*)&P.inst[inst];
+        *ip = (*ip & 0xFFFF000000000000ull) | (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) |
+              ((uint64_t)(q_until & 0xFFFF) << 32);
         P.istats[inst * 4 + 0] += sums[0];
         P.istats[inst * 4 + 1] += sums[1];
         P.istats[inst * 4 + 2] += sums[2];
@@ -934,7 +940,8 @@ int brc_create(const brc_config* cfg, void** out) {
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
     const uint32_t l_words = ((uint32_t)e->dm * 64 * e->msize + 7) / 8;
-    const uint32_t per_wave_words = e->ipw * e->NK + TS * e->nkw + 64 * e->nkw + l_words + (e->ipw * e->NK + 2) / 2 + 1;
+    const uint32_t h_words = (4 * 64 * e->msize + 7) / 8;
+    const uint32_t per_wave_words = e->ipw * e->NK + TS * e->nkw + 64 * e->nkw + l_words + h_words + (e->ipw * e->NK + 2) / 2 + 1;
     e->lds_bytes = per_wave_words * 8 * WPB;
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) { delete e; return BRC_E_INVALID; }
     auto fail = [&](int code) { free_all(e); delete e; return code; };

@@ -61,15 +61,21 @@ def cpu_baseline(seconds):
                       % (count, count - 1, dt, arrivals / dt)}
 
 
-def load_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches."""
+def load_traffic(instances, kernel_ms):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
+    written by profiles/summarize.py), used only if it was taken on this workload and size and
+    its kernel time agrees with the live one within 15 % (i.e. the same kernel build)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        return d
     except (OSError, ValueError):
         return None
+    if d.get("instances") != instances or d.get("workload") != "cfg4" or not d.get("avg_ns"):
+        return None
+    if abs(d["avg_ns"] / 1e6 - kernel_ms) > 0.15 * kernel_ms:
+        return None
+    return d.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -134,10 +140,7 @@ def main():
     out = None
     if rank == 0:
         achieved = SURVEY_BYTES_PER_CELL_STEP * (cell_steps / world) / (kernel_ms / 1e3) / 1e9
-        tr = load_traffic()
-        traffic = None
-        if tr and tr.get("instances") == per and tr.get("workload") == "cfg4":
-            traffic = tr.get("hbm_bytes_per_launch")
+        traffic = load_traffic(per, kernel_ms)
         out = {
             "metric": "decided consensus instances/sec (node) at n=64,f=21",
             "value": value,

@@ -15,5 +15,6 @@ for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $pmc -T -d $OUT/pmc$i -o run --output-format csv -- python3 $BENCH > $OUT/pmc$i.json 2> $OUT/pmc$i.err || { echo "pmc pass $i failed"; exit 1; }
 done
+python3 profiles/summarize.py $OUT profiles/$TAG > $OUT/summary.json || { echo "summary failed"; exit 1; }
 echo "collected $OUT"
 ls -R $OUT | head -40

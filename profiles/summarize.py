@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Summarise a profiles/collect.sh run into committed JSON.
+
+    python profiles/summarize.py gpurun_out/prof_<tag> profiles/<tag> [--kernel brc_kernel]
+
+Writes <dest>/kernel_stats.csv (the rocprofv3 --stats table, copied), <dest>/pmc_summary.json
+(per-kernel mean of every PMC counter over its dispatches) and, for the headline kernel,
+profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+
+HBM bytes follow MI355X_MICROARCH.md (rocprofv3 / HBM section): FETCH_SIZE and WRITE_SIZE are
+in KiB and come from separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of a
+coalesced streaming read, so it is doubled.  The kernel's loads are 8 B/lane coalesced
+512-B wave accesses, where the doubling was checked against SQ_INSTS_VMEM_RD x 512 B.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def load_counters(src):
+    per = defaultdict(lambda: defaultdict(list))
+    for path in sorted(glob.glob(os.path.join(src, "pmc*", "run_counter_collection.csv"))):
+        for r in csv.DictReader(open(path)):
+            per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def kernel_avg_ns(src, kernel):
+    path = os.path.join(src, "trace", "run_kernel_stats.csv")
+    for r in csv.DictReader(open(path)):
+        if r["Name"] == kernel:
+            return float(r["AverageNs"]), int(r["Calls"])
+    return None, 0
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    kernel = "brc_kernel"
+    if "--kernel" in sys.argv:
+        kernel = sys.argv[sys.argv.index("--kernel") + 1]
+        args.remove(kernel)
+    src, dest = args[0], args[1]
+    os.makedirs(dest, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dest, "kernel_stats.csv"))
+    counters = load_counters(src)
+    with open(os.path.join(dest, "pmc_summary.json"), "w") as fh:
+        json.dump(counters, fh, indent=1, sort_keys=True)
+    bench = None
+    bpath = os.path.join(src, "trace_bench.json")
+    if os.path.exists(bpath):
+        bench = json.loads(open(bpath).read().strip().splitlines()[-1])
+        shutil.copy(bpath, os.path.join(dest, "trace_bench.json"))
+    k = counters.get(kernel, {})
+    avg_ns, calls = kernel_avg_ns(src, kernel)
+    out = {"kernel": kernel, "avg_ns": avg_ns, "calls": calls, "source": dest}
+    if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
+        fetch = 2.0 * k["FETCH_SIZE"] * 1024.0
+        write = k["WRITE_SIZE"] * 1024.0
+        out.update({"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
+                    "hbm_gbs": (fetch + write) / avg_ns if avg_ns else None})
+        if "SQ_INSTS_VMEM_RD" in k:
+            out["vmem_rd_bytes_issued"] = k["SQ_INSTS_VMEM_RD"] * 512.0
+            out["vmem_wr_bytes_issued"] = k.get("SQ_INSTS_VMEM_WR", 0.0) * 512.0
+    if bench:
+        cfg = bench.get("config", {})
+        out["instances"] = cfg.get("instances_per_gpu")
+        out["workload"] = cfg.get("workload", "").split(":")[0]
+        out["bench_kernel_ms"] = bench.get("kernel_ms")
+    for path in (os.path.join(dest, "pmc_traffic.json"), os.path.join(os.path.dirname(dest.rstrip("/")), "pmc_traffic.json")):
+        with open(path, "w") as fh:
+            json.dump(out, fh, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

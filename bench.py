@@ -92,13 +92,15 @@ def main():
         dist = tdist
 
     from byzantinerandomizedconsensus_amd import _lib as L
+    from byzantinerandomizedconsensus_amd import shard
     from byzantinerandomizedconsensus_amd.engine import Engine
 
     per = args.instances
-    eng = Engine(n=N_REPLICAS, f=F_FAULTS, instances=per, protocol="consensus", seed=SEED,
+    first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
+    eng = Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
                  delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=1, step_cap=4000,
                  key_window=args.key_window, variants=1, proposals=L.PROPOSALS_PHILOX,
-                 instance_offset=rank * per, device=local)
+                 instance_offset=first, device=local)
 
     def barrier():
         if dist is not None:
@@ -121,19 +123,13 @@ def main():
         kms.append(one_step())
     barrier()
     elapsed = time.perf_counter() - t0
-    st = eng.stats()
-    local_stats = [st["decided"], st["done"], st["overflow"] + st["stepcap"] + st["running"],
-                   st["arrivals"], st["cell_steps"], st["msgs_sent"]]
     kernel_ms = sum(kms) / len(kms)
-    if dist is not None:
-        import torch
-        t = torch.tensor(local_stats, dtype=torch.float64, device="cuda")
-        dist.all_reduce(t)                                   # RCCL over xGMI: statistics only
-        local_stats = [int(x) for x in t.tolist()]
-        m = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(m, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = m.tolist()
-    decided, done, bad, arrivals, cell_steps, msgs = local_stats
+    # the only collective: statistics (RCCL over xGMI), max of the wall clocks
+    st, _ = shard.reduce_stats(eng.stats(), dist, device="cuda")
+    elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
+    kernel_ms = shard.max_over_ranks(kernel_ms, dist, device="cuda")
+    decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
+    bad = st["overflow"] + st["stepcap"] + st["running"]
     if bad:
         print("WARNING: %d instances did not finish cleanly" % bad, file=sys.stderr)
     value = decided * args.steps / elapsed

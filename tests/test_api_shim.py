@@ -1,0 +1,163 @@
+"""The reference's class API on top of the engine.
+
+CPU: import paths, constructor contracts and host-side bookkeeping (no engine launch).
+GPU: reference-style drivers run unchanged and print exactly what the reference's golden
+fixtures say the reference delivers / decides, in the reference's per-step order."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+from byzantinerandomizedconsensus_amd import _lib as L
+from byzantinerandomizedconsensus_amd import network
+from tests import golden_io
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GROUPS = golden_io.groups()
+
+
+@pytest.fixture(autouse=True)
+def fresh_network():
+    network.reset()
+    saved = network.settings()
+    yield
+    network.reset()
+    network.configure(**saved)
+
+
+def test_reference_import_paths():
+    import byzantinerandomizedconsensus  # noqa: F401
+    from byzantinerandomizedconsensus.base.broadcast import Broadcast, IBroadcastHandler
+    from byzantinerandomizedconsensus.base.consensus import Consensus, IConsensusHandler
+    from byzantinerandomizedconsensus.core.brbroadcast import BRBroadcast
+    from byzantinerandomizedconsensus.core.byzantinerandomizedconsensus import ByzantineRandomizedConsensus
+    assert (BRBroadcast.SEND, BRBroadcast.ECHO, BRBroadcast.READY) == (1, 2, 3)
+    assert issubclass(BRBroadcast, Broadcast) and Broadcast.BUFFER_SIZE == 1024
+    assert issubclass(ByzantineRandomizedConsensus, Consensus)
+    assert issubclass(ByzantineRandomizedConsensus, IBroadcastHandler)
+    assert (ByzantineRandomizedConsensus.NONE, ByzantineRandomizedConsensus.PHASE1,
+            ByzantineRandomizedConsensus.PHASE2) == (-1, 1, 2)
+    for iface in (IBroadcastHandler, IConsensusHandler, Consensus):
+        with pytest.raises(TypeError):
+            iface()
+
+
+def _peers(n, port=6000):
+    return [("localhost", port + i) for i in range(n)]
+
+
+def test_constructor_asserts_like_reference():
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    from byzantinerandomizedconsensus_amd.core.byzantinerandomizedconsensus import ByzantineRandomizedConsensus
+    with pytest.raises(AssertionError):
+        BRBroadcast(3, 1, ("localhost", 6000), _peers(3), None)            # core/brbroadcast.py:29
+    with pytest.raises(AssertionError):
+        ByzantineRandomizedConsensus(5, 1, _peers(5, 6100), ("localhost", 6100), None)   # :20
+
+
+def test_brb_sends_become_injections():
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    peers = _peers(4)
+    nodes = [BRBroadcast(4, 1, p, peers, None) for p in peers]
+    for nd in nodes:
+        nd.broadcast_listener()
+    nodes[2].broadcast(BRBroadcast.SEND, "A")
+    nodes[2].broadcast(BRBroadcast.SEND, "A")      # identical message: suppressed by the network
+    nodes[2].broadcast(BRBroadcast.SEND, "B")
+    c = nodes[0].cluster
+    assert all(nd.cluster is c for nd in nodes)
+    assert [(a["node"], a["kp"], a["s"], a["t"]) for a in c.actions] == [(2, 2, 0, 0), (2, 2, 1, 0)]
+    assert c.key_payload == {(2, 0): "A", (2, 1): "B"}
+    with pytest.raises(L.EngineError):
+        nodes[1].broadcast(BRBroadcast.SEND, "A")  # one reference key, two origins
+    with pytest.raises(NotImplementedError):
+        nodes[1].broadcast(BRBroadcast.ECHO, "A")
+    with pytest.raises(ValueError):
+        BRBroadcast(4, 1, ("localhost", 1), peers, None)
+
+
+def test_consensus_values_and_proposals(capsys):
+    from byzantinerandomizedconsensus_amd.core.byzantinerandomizedconsensus import ByzantineRandomizedConsensus
+    peers = _peers(6, 6200)
+    nodes = [ByzantineRandomizedConsensus(6, 1, peers, p, None) for p in peers]
+    for i, nd in enumerate(nodes):
+        nd.message_queue.put_nowait(i % 2)
+        nd.start()
+    out = capsys.readouterr().out.splitlines()
+    assert out[0] == "Consensus started on ('localhost', 6200)" and out[1] == "Proposal sent on ('localhost', 6200)"
+    c = nodes[0].brb.cluster
+    assert c.mode == "consensus"
+    assert [(a["node"], a["value"]) for a in c.actions] == [(i, 1 + i % 2) for i in range(6)]
+    assert c.values.strings == ["-1", "0", "1"]
+    assert nodes[3].round == 1 and nodes[3].phase == 1
+
+
+def test_value_table_limits():
+    vt = network.ValueTable()
+    assert [vt.id_of(x) for x in ("-1", "a", 3, "a", "3", "b")] == [0, 1, 2, 1, 2, 3]
+    with pytest.raises(L.EngineError):
+        vt.id_of("c")
+
+
+def test_step_event_order():
+    evs = [(L.EV_DELIVER, 2, 0, 0), (L.EV_DELIVER, 0, 3, 0), (L.EV_DELIVER, 0, 1, 1), (L.EV_DELIVER, 0, 1, 0)]
+    assert network.order_step_events(evs) == [(1, 0, 1, 0), (1, 0, 1, 1), (1, 0, 3, 0), (1, 2, 0, 0)]
+
+
+# ---------------------------------------------------------------------------------- GPU
+def _run_driver(name):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "drivers", name)], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    return out.stdout.splitlines()
+
+
+@pytest.mark.gpu
+def test_brb_driver_unchanged_matches_reference():
+    # FIFO n=4 f=1, every node SENDs at once -> 16 deliveries
+    case = GROUPS["brb_fifo_n4"][0]
+    exp = ["TEST %d" % (kp + 1) for (_t, _node, kp, _s) in case["result"]["events"]["deliver"]]
+    assert _run_driver("brb_driver.py") == exp
+
+
+@pytest.mark.gpu
+def test_brc_driver_unchanged_matches_reference():
+    case = GROUPS["cons_brc_test_n6"][0]
+    head = []
+    for i in range(6):
+        head += ["Consensus started on ('localhost', %d)" % (5555 + i), "Proposal sent on ('localhost', %d)" % (5555 + i)]
+    exp = head + ["Consensus protocol decided on message: " + v for (_t, _n, _r, v) in case["result"]["events"]["decide"]]
+    assert _run_driver("brc_driver.py") == exp
+
+
+@pytest.mark.gpu
+def test_upcall_order_and_steps_match_reference():
+    """Every upcall at the step and in the per-step order the reference produces (uniform
+    random delays: deliveries of several keys interleave across steps)."""
+    from byzantinerandomizedconsensus_amd.base.broadcast import IBroadcastHandler
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    for case in GROUPS["brb_uniform_n10"][:3]:
+        sp = case["spec"]
+        network.reset()
+        network.configure(delay_model=sp["delay_model"], delay_max=sp["dmax"], seed=sp["seed"],
+                          instance_id=sp["g"])
+        got = []
+
+        class H(IBroadcastHandler):
+            def __init__(self, i):
+                self.i = i
+
+            def deliver(self, message):
+                got.append([cluster.t, self.i, message])
+
+        peers = _peers(sp["n"], 6300)
+        nodes = [BRBroadcast(sp["n"], sp["f"], p, peers, H(i)) for i, p in enumerate(peers)]
+        cluster = nodes[0].cluster
+        for a in sp["actions"]:
+            assert a["kind"] == "brb_send" and a["t"] == 0
+            nodes[a["node"]].broadcast(BRBroadcast.SEND, a["payload"])
+        cluster.run()
+        exp = [[t, node, "TEST %d.%d" % (kp + 1, s)] for (t, node, kp, s) in case["result"]["events"]["deliver"]]
+        assert got == exp

@@ -1,31 +1,13 @@
-// brc_engine.hip -- MI355X (gfx950) batched Bracha-broadcast + randomized-consensus engine.
+// brc_engine.hip -- host side of the MI355X batched consensus engine: the C-ABI of
+// include/brc.h (brc_create ... brc_destroy), device memory, injection CSR upload, and the small
+// helper kernels.  The step kernel itself is brc_step.h, instantiated per replica-set width in
+// brc_kern_<NPAD>.hip.
 //
-// One 64-lane wavefront simulates an "item": IPW = 64 / NPAD independent instances, lane =
-// (instance segment, replica).  Lane d is at once receiver d (its BRB cells), sender d (its
-// send steps are read back by every receiver through __ballot) and consensus replica d.  A
-// wave runs its item from the current step to completion in ONE launch: instances are
-// independent, so no inter-wave communication exists at all.  Workgroups hold 4 such waves
-// that never synchronise with each other (LDS is partitioned per wave).
-//
-// Hot path replaced (reference = sithu/ByzantineRandomizedConsensus):
-//   brb_cell_update()  <- core/brbroadcast.py:60-119  (per-message handler, batched per step)
-//   consensus pass     <- core/byzantinerandomizedconsensus.py:53-106 (deliver / get_max_val)
-//   send_key()         <- core/byzantinerandomizedconsensus.py:43-51, base/broadcast.py:17-40
-//
-// Cell = (receiver, key).  The network suppresses duplicates (oracle/schedule.py), so every
-// ECHO/READY that reaches a cell comes from a new sender: the reference's sets
-// (core/brbroadcast.py:38-41) only ever matter through their sizes, and a cell is one word:
-//   bits  0- 4 flags  (entry in echo_sent_list, entry in ready_sent_list, delivered,
-//                      ECHO sent, READY sent)
-//   bits  5-11 |echo set|      bits 12-18 |ready set|     bits 19-31 allocation generation
-//   bits 32-47 step this lane SENT its ECHO of the key     bits 48-63 ... its READY (0xFFFF: never)
-// HBM (lane-contiguous => every access is one coalesced 512-B wave access):
-//   cells [item][NK][64] u64
-// per instance key slots (copied to LDS for the launch): meta [inst][NK] u64 (s+1 | t_send |
-//   t_quiet | sender | value), mgen [inst][NK] u32 (generation | restricted-SEND flag),
-//   kdst [inst][NK] u64 (SEND destinations, read only for restricted SENDs)
-// per item: act [item][32][nkw] u64 (key slots that may have arrivals at step t mod 32)
-// per lane: cons0/cons1 [item][64] u64, hmask [item][4][64] T (consensus state)
+// Reference boundary replaced (sithu/ByzantineRandomizedConsensus):
+//   BRBroadcast / ByzantineRandomizedConsensus constructors  -> brc_create
+//   the listener accept loop (core/brbroadcast.py:60-128)     -> brc_run (one step-kernel launch)
+//   Broadcast.broadcast / Consensus.propose                   -> brc_inject / brc_load_proposals
+//   deliver / decide upcalls                                  -> brc_read_events / brc_read_replicas
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -35,663 +17,11 @@
 #include <string>
 #include <vector>
 
-#include "../../include/brc.h"
-#include "schedule.h"
+#include "brc_internal.h"
 
 namespace {
 
-constexpr int TS = 32;            // activity ring (steps); > max delay
-constexpr int WPB = 4;            // independent waves per workgroup
-#ifndef BRC_CHUNK
-#define BRC_CHUNK 8
-#endif
-constexpr int CHUNK = BRC_CHUNK;  // key slots processed together (memory-level parallelism)
-constexpr uint32_t NEVER = 0xFFFFu;
-constexpr uint64_t TIMES_NEVER = 0xFFFFFFFF00000000ull;
-constexpr uint32_t F_EEX = 1, F_REX = 2, F_DEL = 4, F_ES = 8, F_RS = 16;
-constexpr uint32_t GEN_MASK = 0x1FFF;
-constexpr uint32_t GEN_RESTRICTED = 0x80000000u;
-constexpr uint32_t STEP_LIMIT = 60000;
-constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
-
-struct InjDev {       // 24 B, per item CSR, sorted by t
-    uint32_t t;
-    uint16_t slot, s;
-    uint8_t kind, type, seg, node;
-    int8_t value;
-    uint8_t pad[3];
-    uint64_t dst;
-};
-
-struct ItemState { uint32_t t, inj_pos, initialized, pad; };
-
-struct InstState { uint16_t status, t_stop, q_until, flags; uint32_t pad0, pad1; };
-
-struct Params {
-    uint32_t n, f, D, Q, NV, NK, nkw;
-    uint32_t protocol, delay_model, dconst, round_cap, step_cap, proposals;
-    uint32_t T_echo, T_amp, T_del, T_cnt, bound_p1, bound_p2;
-    uint64_t seed, inst_offset, instances, nitems;
-    uint32_t max_steps, pad;
-    uint64_t event_cap;
-    uint64_t* cells;
-    uint64_t* meta; uint32_t* mgen; uint64_t* kdst;
-    uint64_t* act; uint32_t* actany; ItemState* items; InstState* inst; uint64_t* istats;
-    uint64_t* cons0; uint64_t* cons1; void* hmask;
-    const InjDev* inj; const uint32_t* inj_off; const uint32_t* inj_cnt;
-    const uint64_t* byz; const int8_t* prop;
-    brc_event* events; unsigned long long* event_count;
-    unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
-};
-
-template <int NPAD> struct MaskOf { using type = uint64_t; };
-template <> struct MaskOf<4> { using type = uint8_t; };
-template <> struct MaskOf<8> { using type = uint8_t; };
-template <> struct MaskOf<16> { using type = uint16_t; };
-template <> struct MaskOf<32> { using type = uint32_t; };
-
-template <int NPAD> constexpr int nkw_of() { return NPAD / 8 < 1 ? 1 : NPAD / 8; }   // NK <= 8 * NPAD
-
-template <typename T> __device__ __forceinline__ uint32_t popc(T x) { return (uint32_t)__popcll((uint64_t)x); }
-
-__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
-#pragma unroll
-    for (int o = 32; o; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o);
-    return x;
-}
-
-template <int NPAD> __device__ __forceinline__ uint32_t seg_max(uint32_t x) {
-#pragma unroll
-    for (int o = NPAD / 2; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
-    return x;
-}
-
-template <int NPAD, typename T> __device__ __forceinline__ T seg_or(T x) {
-#pragma unroll
-    for (int o = NPAD / 2; o; o >>= 1) x |= (T)__shfl_xor((unsigned long long)x, o);
-    return x;
-}
-
-__device__ __forceinline__ uint32_t hibit(uint32_t x) { return x ? 32u - (uint32_t)__clz(x) : 0u; }
-
-// compile-time unrolled loop: f(IC<0>{}), ..., f(IC<N-1>{}) (register arrays stay statically indexed)
-template <int I> struct IC { static constexpr int value = I; };
-template <int N> struct Unrolled {
-    template <typename F> __device__ __forceinline__ static void run(F&& f) {
-        Unrolled<N - 1>::run(f);
-        f(IC<N - 1>{});
-    }
-};
-template <> struct Unrolled<0> {
-    template <typename F> __device__ __forceinline__ static void run(F&&) {}
-};
-
-// wave-uniform value -> scalar registers (valid only when every lane holds the same value)
-__device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-    return (uint64_t)uni32((uint32_t)x) | ((uint64_t)uni32((uint32_t)(x >> 32)) << 32);
-}
-
-// packed LDS/HBM key metadata
-__device__ __forceinline__ uint32_t m_s1(uint64_t m) { return (uint32_t)(m & 0xFFFF); }
-__device__ __forceinline__ uint32_t m_tsend(uint64_t m) { return (uint32_t)((m >> 16) & 0xFFFF); }
-__device__ __forceinline__ uint32_t m_tquiet(uint64_t m) { return (uint32_t)((m >> 32) & 0xFFFF); }
-__device__ __forceinline__ uint32_t m_sender(uint64_t m) { return (uint32_t)((m >> 48) & 0xFF); }
-__device__ __forceinline__ uint32_t m_value(uint64_t m) { return (uint32_t)((m >> 56) & 0xFF); }
-__device__ __forceinline__ uint64_t m_pack(uint32_t s1, uint32_t tsend, uint32_t tquiet, uint32_t sender, uint32_t value) {
-    return (uint64_t)(s1 & 0xFFFF) | ((uint64_t)(tsend & 0xFFFF) << 16) | ((uint64_t)(tquiet & 0xFFFF) << 32) |
-           ((uint64_t)(sender & 0xFF) << 48) | ((uint64_t)(value & 0xFF) << 56);
-}
-__device__ __forceinline__ uint64_t m_with_tquiet(uint64_t m, uint32_t q) {
-    return (m & ~(0xFFFFull << 32)) | ((uint64_t)(q & 0xFFFF) << 32);
-}
-
-// core/brbroadcast.py:60-119 for ONE (receiver, key) cell and every message reaching it in one
-// step, in the canonical order SEND, ECHO by sender ascending, READY by sender ascending.  All
-// arrivals grow their set (duplicates are suppressed), so the sequential threshold crossings
-// have closed forms in the set sizes:
-//   ECHO  : the first ECHO of a missing entry creates it WITHOUT the quorum check (:87-89);
-//           every later one is checked (:92-98), the last checked size is |E| after the step.
-//   READY : same creation quirk (:103-105); checked sizes run lo..hi; DELIVER at the first size
-//           >= 2f+1 (:111-115); amplification (:118-119) fires for checked sizes in [f+1, 2f]
-//           while no ECHO entry exists -- only its first firing leaves the node (duplicates).
-__device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint32_t& rc, bool s_arr,
-                                                uint32_t ea, uint32_t ra, uint32_t T_echo, uint32_t T_amp,
-                                                uint32_t T_del, bool& echo_send, bool& ready_send, bool& deliver) {
-    echo_send = ready_send = deliver = false;
-    if (fl & F_DEL) return;                                              // :74
-    if (s_arr && !(fl & F_EEX)) { fl |= F_EEX | F_ES; echo_send = true; }   // :76-82
-    if (ea) {
-        uint32_t checked = ea;
-        if (!(fl & F_EEX)) { fl |= F_EEX; checked = ea - 1; }           // :87-89
-        ec += ea;                                                        // :89/:92
-        if (checked && ec >= T_echo && !(fl & F_REX)) { fl |= F_REX | F_RS; ready_send = true; }   // :95-98
-    }
-    if (ra) {
-        uint32_t lo, hi;
-        if (!(fl & F_REX)) { fl |= F_REX; lo = 2; hi = ra; }            // :103-105
-        else { lo = rc + 1; hi = rc + ra; }                              // :108
-        rc += ra;
-        if (hi >= lo) {
-            if (!(fl & F_EEX)) {                                         // :118
-                const uint32_t alo = max(lo, T_amp), ahi = min(hi, T_del - 1);
-                if (alo <= ahi && !(fl & F_RS)) { fl |= F_RS; ready_send = true; }   // :119
-            }
-            if (hi >= T_del) { fl |= F_DEL; deliver = true; }            // :111-115
-        }
-    }
-}
-
-#ifndef BRC_MIN_WAVES
-#define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
-#endif
-
-template <int NPAD, int DM>
-__global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_kernel(Params P) {
-    using T = typename MaskOf<NPAD>::type;
-    constexpr int IPW = 64 / NPAD;
-    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-
-    const int wid = threadIdx.x / 64, lane = threadIdx.x % 64;
-    const uint64_t item = (uint64_t)blockIdx.x * WPB + wid;
-    if (item >= P.nitems) return;               // whole wave exits; waves never synchronise
-    const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
-    // per-wave LDS carve: meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 |
-    //                     L[DM][64] T | hm[4][64] T | mgen[IPW*NK] u32 | any u32
-    const uint32_t l_words = (DM * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    const uint32_t h_words = (4 * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    const uint32_t per_wave_words = IPW * NK + TS * nkw + 64 * nkw + l_words + h_words + (IPW * NK + 2) / 2 + 1;
-    uint64_t* s_meta = smem + (size_t)wid * per_wave_words;
-    uint64_t* s_act = s_meta + IPW * NK;
-    uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
-    T* s_L = (T*)(s_dbits + 64 * nkw);           // s_L[i*64 + lane]: senders at delay i+1
-    T* s_hm = (T*)(s_dbits + 64 * nkw + l_words);   // s_hm[v*64 + lane]: hosts that delivered value v
-    uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + l_words + h_words);
-    uint32_t* s_any = s_gen + IPW * NK;
-
-    const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
-    const uint64_t inst = item * IPW + seg;
-    const bool iex = inst < P.instances;
-    const uint64_t g = P.inst_offset + inst;
-    const uint64_t all64 = (n >= 64) ? ~0ull : ((1ull << n) - 1);
-    const T allm = (T)all64;
-    const uint64_t segbits = (NPAD == 64) ? ~0ull : (((1ull << NPAD) - 1) << segbase);
-    const uint32_t mbase = seg * NK;             // this lane's instance in the LDS meta arrays
-
-    ItemState its = P.items[item];
-    uint32_t t = its.t, inj_pos = its.inj_pos;
-    const uint32_t inj_off = P.inj_off[item], inj_cnt = P.inj_cnt[item];
-    {
-        const uint64_t mb = item * IPW * (uint64_t)NK;
-        for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            const bool ok = item * IPW + i / NK < P.instances;
-            s_meta[i] = ok ? P.meta[mb + i] : 0ull;
-            s_gen[i] = ok ? P.mgen[mb + i] : 0u;
-        }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) s_act[i] = P.act[item * TS * nkw + i];
-        for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
-        if (lane == 0) *s_any = P.actany[item];
-    }
-
-    uint32_t status = BRC_DONE, t_stop = 0, q_until = 0;
-    if (iex) {
-        const uint64_t w0 = *(const uint64_t*)&P.inst[inst];     // status | t_stop | q_until | flags
-        status = w0 & 0xFFFF; t_stop = (w0 >> 16) & 0xFFFF; q_until = (w0 >> 32) & 0xFFFF;
-    }
-    const uint64_t byzm = iex ? P.byz[inst] : ~0ull;
-    const bool real = iex && (uint32_t)d < n;
-    const bool honest = real && !((byzm >> d) & 1ull);
-
-    // ---- link-delay masks: L[i] = senders j whose link j -> d has delay i+1 (schedule.h)
-    T L[DM];
-#pragma unroll
-    for (int i = 0; i < DM; ++i) L[i] = 0;
-    if (real) {
-        if (P.delay_model == BRC_DELAY_CONST) {
-#pragma unroll
-            for (int i = 0; i < DM; ++i) if ((uint32_t)i + 1 == P.dconst) L[i] = allm;
-        } else if (P.delay_model == BRC_DELAY_SLOWSET) {
-            const uint32_t off = brc::slow_offset(P.seed, g, n);
-            T slowm = 0;
-            for (uint32_t j = 0; j < n; ++j) if (((j + n - off) % n) < P.f) slowm |= (T)((T)1 << j);
-            const bool me_slow = ((uint32_t)d + n - off) % n < P.f;
-#pragma unroll
-            for (int i = 0; i < DM; ++i) {
-                if ((uint32_t)i + 1 == D) L[i] |= me_slow ? allm : slowm;
-                if (i == 0) L[i] |= me_slow ? (T)0 : (T)(allm & ~slowm);
-            }
-        } else {
-            for (uint32_t j4 = 0; j4 < (n + 3) / 4; ++j4) {
-                const brc::u32x4 w = brc::draw(P.seed, g, (uint32_t)d, brc::PURPOSE_DELAY, j4);
-                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t j = 4 * j4 + q;
-                    if (j >= n) break;
-                    const uint32_t dl = (P.delay_model == BRC_DELAY_UNIFORM) ? brc::uniform_delay(ws[q], D)
-                                                                             : brc::geometric_delay(ws[q], D);
-#pragma unroll
-                    for (int i = 0; i < DM; ++i) if ((uint32_t)i + 1 == dl) L[i] |= (T)((T)1 << j);
-                }
-            }
-        }
-    }
-    // outset: delays (bit i <=> delay i+1) from THIS lane, as a sender, to honest receivers
-    uint32_t outset = 0;
-#pragma unroll
-    for (int i = 0; i < DM; ++i) {
-        const T m = seg_or<NPAD, T>(honest ? L[i] : (T)0);
-        if (real && ((m >> d) & 1)) outset |= 1u << i;
-        s_L[i * 64 + lane] = L[i];
-    }
-    const uint32_t maxout = hibit(outset);
-    const uint32_t dset = uni32(wave_or(outset));    // every delay some link of this wave has
-    uint64_t* const mycells = P.cells + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
-
-    // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
-    uint64_t c0 = 0, c1 = 0;
-    const size_t li = item * 64 + lane;
-    const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
-    if (cons_lane) { c0 = P.cons0[li]; c1 = P.cons1[li]; }
-    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? ((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
-    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
-    uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
-    uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
-    uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
-
-    uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
-    bool ovf = false, badinj = false;
-
-    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b) {
-        if (P.event_cap) {
-            const unsigned long long i = atomicAdd(P.event_count, 1ull);
-            if (i < P.event_cap) {
-                brc_event e;
-                e.instance = inst; e.t = t; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
-                e.type = (uint8_t)type; e.pad = 0; e.a = a; e.b = b;
-                P.events[i] = e;
-            }
-        }
-    };
-    auto mark = [&](uint32_t k, uint32_t dset) {   // key k may have arrivals at t + delay
-        while (dset) {
-            const uint32_t i = __ffs(dset) - 1; dset &= dset - 1;
-            const uint32_t row = (t + i + 1) & (TS - 1);
-            atomicOr((unsigned long long*)&s_act[row * nkw + (k >> 6)], 1ull << (k & 63));
-            atomicOr(s_any, 1u << row);
-        }
-    };
-    // honest origin d broadcasts SEND for its key (d, s) with value v
-    // (core/byzantinerandomizedconsensus.py:48-50 / :80-83 / :102-106, base/broadcast.py:30-35)
-    auto send_key = [&](uint32_t s, uint32_t v) {
-        const uint32_t k = (d * NV) * Q + (s % Q);
-        const uint64_t m = s_meta[mbase + k];
-        if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
-        s_gen[mbase + k] = ((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK;
-        s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
-        mark(k, outset);
-        q_until = max(q_until, t + maxout);
-        st_msgs += n;
-        st_smax = max(st_smax, s);
-        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
-    };
-    auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
-        for (uint32_t i = 0; i < nvals; ++i) {
-            const uint32_t v = (order >> (2 * i)) & 3;
-            if (2 * popc(s_hm[v * 64 + lane]) > bound2) return v;
-        }
-        return 0;                                                    // str(NONE) == "-1"
-    };
-    auto cons_reset = [&]() {
-        vcount = 0; nvals = 0; order = 0;
-        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
-    };
-    auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = (k / Q) / NV;
-        bool found = false;
-        for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
-        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
-        s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
-        ++vcount;                                                    // :61
-        if (vcount >= P.T_cnt && phase == 1) {                       // :71
-            const uint32_t prop = get_max_val(P.bound_p1);           // :73
-            phase = 2; cons_reset();                                 // :75-78
-            send_key(2 * (round - 1) + 1, prop);                     // :80-83
-        }
-        if (vcount >= P.T_cnt && phase == 2) {                       // :86
-            const uint32_t dec = get_max_val(P.bound_p2);            // :88
-            // :89 compares str with int: never equal -> decide() always runs (:94)
-            ++dcount;
-            if (dcount == 1) { frnd = round; ft = t; fval = dec; }
-            lval = dec;
-            log_ev(BRC_EV_DECIDE, d, 0, round, dec);
-            ++round; phase = 1; cons_reset();                        // :96-100
-            send_key(2 * (round - 1), dec);                          // :102-106
-        }
-    };
-
-    // ---- actions stamped t (performed after step t's messages)
-    auto do_actions = [&]() -> bool {
-        bool mine_any = false;
-        const bool running = status == BRC_RUNNING;
-        if (its.initialized == 0 && t == 0) {
-            if (P.protocol == BRC_PROTO_CONSENSUS && P.proposals != BRC_PROPOSALS_NONE && honest && running) {
-                const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? brc::proposal_id(P.seed, g, d)
-                                                                         : (uint32_t)P.prop[inst * n + d];
-                round = 1; phase = 1;                                 // :43-47
-                send_key(0, v & 3);
-            }
-        }
-        while (inj_pos < inj_cnt) {
-            const InjDev r = P.inj[inj_off + inj_pos];
-            if (r.t != t) break;
-            ++inj_pos;
-            const bool mine = running && seg == (int)r.seg;
-            mine_any |= mine;
-            if (r.kind == BRC_INJ_PROPOSE) {
-                if (mine && honest && d == r.node) { round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3); }
-            } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
-                // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the
-                // slot first unless that key was declared and not yet sent
-                const bool is_send = r.kind == BRC_INJ_SEND;
-                uint32_t myset = 0;
-                if (is_send && mine && honest && ((r.dst >> d) & 1ull)) {
-                    for (uint32_t i = 0; i < D; ++i) if ((s_L[i * 64 + lane] >> r.node) & 1) myset = 1u << i;
-                }
-                const uint32_t os = wave_or(myset);
-                if (mine) {
-                    const uint32_t k = r.slot;
-                    if (d == 0) {
-                        uint64_t m = s_meta[mbase + k];
-                        uint32_t gen = s_gen[mbase + k] & GEN_MASK;
-                        const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
-                        if (!declared && m_s1(m) != 0 && t < m_tquiet(m)) {
-                            ovf = true;
-                        } else {
-                            uint32_t tq = m_tquiet(m);
-                            // a declared key holds its slot at least until the next step
-                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; }
-                            if (is_send) tq = max(tq, t + hibit(os));
-                            m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
-                            s_meta[mbase + k] = m;
-                            const bool restricted = is_send && (r.dst & all64) != all64;
-                            s_gen[mbase + k] = gen | (restricted ? GEN_RESTRICTED : 0u);
-                            st_smax = max(st_smax, (uint32_t)r.s);
-                            if (is_send) {
-                                P.kdst[inst * NK + k] = r.dst;
-                                mark(k, os);
-                                st_msgs += __popcll(r.dst & all64);
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
-                            }
-                        }
-                    }
-                    q_until = max(q_until, t + hibit(os));
-                }
-            } else if (r.kind == BRC_INJ_MSG) {
-                const uint32_t k = r.slot;
-                bool sent = false;
-                if (mine && d == r.node) {
-                    const uint64_t m = s_meta[mbase + k];
-                    if (m_s1(m) != r.s + 1u) {
-                        badinj = true;
-                    } else {
-                        const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
-                        const size_t ci = ((size_t)item * NK + k) * 64 + lane;
-                        uint64_t wv = P.cells[ci];
-                        if (((wv >> 19) & GEN_MASK) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 19);
-                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
-                        if (!(wv & bit)) {
-                            sent = true;
-                            wv |= bit;
-                            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
-                            wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            P.cells[ci] = wv;
-                            st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
-                        }
-                    }
-                }
-                const uint32_t os = wave_or(sent ? outset : 0u);
-                if (os) {
-                    if (lane == 0) mark(k, os);
-                    const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
-                    if (mine && myq) {
-                        if (d == 0) {
-                            const uint64_t m = s_meta[mbase + k];
-                            if (myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
-                        }
-                        q_until = max(q_until, myq);
-                    }
-                }
-            }
-        }
-        its.initialized = 1;
-        return mine_any;
-    };
-
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (its.initialized == 0 && t == 0) {
-        do_actions();
-        q_until = seg_max<NPAD>(q_until);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-
-    for (uint32_t it = 0; it < P.max_steps; ++it) {
-        const bool running = status == BRC_RUNNING;
-        if (!__any(running)) break;
-        // next step with possible arrivals (activity ring) or a pending action
-        const uint32_t any = *s_any;
-        const uint32_t rot = (t + 1) & (TS - 1);
-        const uint32_t rr = rot ? ((any >> rot) | (any << (TS - rot))) : any;
-        uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
-        if (inj_pos < inj_cnt) next = min(next, P.inj[inj_off + inj_pos].t);
-        if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
-        if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
-        t = next;
-        const uint32_t row = t & (TS - 1);
-
-        // ================= BRB: active key slots in chunks; one (receiver, key) cell per lane
-        bool lane_active = false, any_del = false;
-#pragma unroll 1
-        for (uint32_t w = 0; w < nkw; ++w) {
-            uint64_t rem = uni64(s_act[row * nkw + w]);
-            while (rem) {
-                uint32_t kc[CHUNK];
-                bool vc[CHUNK];
-                uint64_t wc[CHUNK];
-                // phase A: every lane's cell word of CHUNK key slots, all loads in flight at once
-                Unrolled<CHUNK>::run([&](auto ci) {
-                    constexpr int c = decltype(ci)::value;
-                    vc[c] = rem != 0;
-                    kc[c] = w * 64 + (vc[c] ? (uint32_t)(__ffsll((unsigned long long)rem) - 1) : 0u);
-                    rem &= rem - 1;
-                    wc[c] = vc[c] ? mycells[(size_t)kc[c] * 64] : TIMES_NEVER;
-                });
-                // phase B: arrivals (ballots over senders), closed-form update, sends
-                Unrolled<CHUNK>::run([&](auto ci) {
-                    constexpr int c = decltype(ci)::value;
-                    if (!vc[c]) return;
-                    const uint32_t k = kc[c];
-                    uint64_t m = s_meta[mbase + k];
-                    uint32_t gw = s_gen[mbase + k];
-                    if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
-                    const bool live = running && m_s1(m) != 0;
-                    const uint64_t word = (live && real) ? wc[c] : TIMES_NEVER;
-                    const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
-                    const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
-                    uint32_t ea = 0, ra = 0;
-                    for (uint32_t ds = dset; ds; ds &= ds - 1) {         // only delays some link has
-                        const uint32_t i = __ffs(ds) - 1;
-                        const uint64_t be = __ballot(dE == i + 1), br = __ballot(dR == i + 1);
-                        if (be | br) {
-                            const T Li = s_L[i * 64 + lane];
-                            ea += popc((T)(be >> segbase) & Li);
-                            ra += popc((T)(br >> segbase) & Li);
-                        }
-                    }
-                    bool s_arr = false;
-                    if (live && honest) {
-                        const uint32_t dt = t - m_tsend(m);
-                        if (dt >= 1 && dt <= D) {
-                            const bool to_me = !(gw & GEN_RESTRICTED) || ((P.kdst[inst * NK + k] >> d) & 1ull);
-                            s_arr = to_me && ((s_L[(dt - 1) * 64 + lane] >> m_sender(m)) & 1);
-                        }
-                    }
-                    const bool has = live && honest && (s_arr || ea || ra);
-                    bool echo_send = false, ready_send = false, deliver = false;
-                    st_loads += (live && real) ? 1u : 0u;
-                    if (has) {
-                        const uint32_t gen = gw & GEN_MASK;
-                        uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
-                        uint32_t tEn = tE, tRn = tR;
-                        if ((((uint32_t)word >> 19) & GEN_MASK) != gen) { fl = 0; ec = 0; rc = 0; tEn = NEVER; tRn = NEVER; }
-                        brb_cell_update(fl, ec, rc, s_arr, ea, ra, P.T_echo, P.T_amp, P.T_del,
-                                        echo_send, ready_send, deliver);
-                        if (echo_send) tEn = t;
-                        if (ready_send) tRn = t;
-                        mycells[(size_t)k * 64] =
-                            (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) | ((uint64_t)gen << 19) |
-                            ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
-                        st_arr += ea + ra + (s_arr ? 1u : 0u);
-                        st_cells += 1;
-                        if (echo_send) st_msgs += n;
-                        if (ready_send) st_msgs += n;
-                        if (deliver) {
-                            st_del += 1; any_del = true;
-                            s_dbits[w * 64 + lane] |= 1ull << (k & 63);
-                        }
-                        if (P.event_cap) {
-                            const uint32_t kp = k / Q, s = m_s1(m) - 1u;
-                            if (echo_send) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
-                            if (ready_send) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
-                            if (deliver) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
-                        }
-                    }
-                    lane_active |= has;
-                    const bool sent = echo_send || ready_send;
-                    if (__ballot(sent)) {
-                        const uint32_t os = wave_or(sent ? outset : 0u);
-                        if (lane == 0) mark(k, os);
-                        const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
-                        if (live && myq) {
-                            if (d == 0 && myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
-                            q_until = max(q_until, myq);
-                        }
-                    }
-                });
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-
-        // ================= consensus: this step's deliveries in canonical (kp, s) order
-        if (any_del) {
-            const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
-            const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
-#pragma unroll 1
-            for (uint32_t w = 0; w < nkw; ++w) {
-                uint64_t bits = s_dbits[w * 64 + lane];
-                s_dbits[w * 64 + lane] = 0;
-                if (!cons) bits = 0;
-                while (bits) {
-                    const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
-                    const uint32_t base = b0 - (b0 % Q);
-                    uint64_t grp = bits & (gm0 << base);
-                    bits &= ~(gm0 << base);
-                    while (grp) {          // several phase indices of one origin: ascending s
-                        uint32_t best = __ffsll((unsigned long long)grp) - 1;
-                        if (grp & (grp - 1)) {
-                            uint32_t bs = 0xFFFFFFFFu;
-                            for (uint64_t x = grp; x; x &= x - 1) {
-                                const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                                const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
-                                if (s1 < bs) { bs = s1; best = bb; }
-                            }
-                        }
-                        grp &= ~(1ull << best);
-                        cons_deliver(w * 64 + best);
-                    }
-                }
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-
-        // ================= actions stamped t
-        const bool inj_mine = do_actions();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-
-        // ================= per-instance stop conditions
-        q_until = seg_max<NPAD>(q_until);
-        const uint64_t b_act = __ballot(lane_active || inj_mine) & segbits;
-        const uint64_t b_ovf = __ballot(ovf) & segbits;
-        const uint64_t b_bad = __ballot(badinj) & segbits;
-        const uint64_t b_und = __ballot(honest && dcount < P.round_cap) & segbits;
-        if (running) {
-            if (b_act) t_stop = t;
-            if (b_bad) status = BRC_BADINJ;
-            else if (b_ovf) status = BRC_OVERFLOW;
-            else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !b_und) status = BRC_DONE;
-            else if (q_until <= t) {
-                bool pending = false;
-                for (uint32_t p = inj_pos; p < inj_cnt && !pending; ++p) pending = P.inj[inj_off + p].seg == (uint32_t)seg;
-                if (!pending) status = BRC_QUIESCENT;
-            }
-        }
-        if ((uint32_t)lane < nkw) s_act[row * nkw + lane] = 0;
-        if (lane == 0) atomicAnd(s_any, ~(1u << row));
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
-
-    // ---- write back
-    {
-        const uint64_t mb = item * IPW * (uint64_t)NK;
-        for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            if (item * IPW + i / NK < P.instances) { P.meta[mb + i] = s_meta[i]; P.mgen[mb + i] = s_gen[i]; }
-        }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) P.act[item * TS * nkw + i] = s_act[i];
-    }
-    if (lane == 0) {
-        P.actany[item] = *s_any;
-        ItemState o = {t, inj_pos, 1u, 0u};
-        P.items[item] = o;
-    }
-    if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
-        P.cons0[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
-                      ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
-        P.cons1[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
-                      ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
-        for (int v = 0; v < 4; ++v) ((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
-    }
-    // statistics: reduce over the segment, its leader writes the instance row
-    uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-        for (int o = NPAD / 2; o; o >>= 1) sums[q] += (uint32_t)__shfl_xor((int)sums[q], o);
-    }
-    if (iex && d == 0) {
-        uint64_t* ip = (uint64_t*)&P.inst[inst];
-        *ip = (*ip & 0xFFFF000000000000ull) | (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) |
-              ((uint64_t)(q_until & 0xFFFF) << 32);
-        P.istats[inst * 4 + 0] += sums[0];
-        P.istats[inst * 4 + 1] += sums[1];
-        P.istats[inst * 4 + 2] += sums[2];
-        P.istats[inst * 4 + 3] += sums[3];
-    }
-    uint64_t w6[5] = {st_cells, st_arr, st_msgs, st_del, st_loads};
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-#pragma unroll
-        for (int o = 32; o; o >>= 1) w6[q] += (uint64_t)__shfl_xor((unsigned long long)w6[q], o);
-    }
-    uint32_t smax = st_smax;
-#pragma unroll
-    for (int o = 32; o; o >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o));
-    if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < 5; ++q) if (w6[q]) atomicAdd(&P.gcount[q], (unsigned long long)w6[q]);
-        if (smax) atomicMax(&P.gcount[5], (unsigned long long)smax);
-    }
-}
+using namespace brc;
 
 // Byzantine equivocation pattern expanded straight into the CSR lists.
 __global__ void expand_equivocate(InjDev* inj, uint32_t* off, uint32_t* cnt, const uint64_t* byz,
@@ -731,11 +61,12 @@ __global__ void expand_equivocate(InjDev* inj, uint32_t* off, uint32_t* cnt, con
     cnt[item] = c;
 }
 
-// brc_reset: free every slot but keep its generation; drop every stored send step.
-__global__ void reset_slots(uint64_t* meta, uint32_t* mgen, uint64_t keys, uint64_t* cells, uint64_t ncells) {
+// brc_reset: free every slot but keep its generation.  Cells are left alone: the next
+// allocation of a slot bumps its generation, which makes every cell of the old key stale
+// (send steps included, brc_step.h), so a reset costs O(keys), not O(cells).
+__global__ void reset_slots(uint64_t* meta, uint32_t* mgen, uint64_t keys) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < keys) { meta[i] = 0; mgen[i] &= GEN_MASK; }
-    if (i < ncells) cells[i] = (cells[i] & 0xFFFFFFFFull) | TIMES_NEVER;
 }
 
 __global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
@@ -785,20 +116,15 @@ static int pick_npad(uint32_t n) {
 
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
-template <typename F>
-static int dispatch(int npad, int dm, F&& f) {
-#define BRC_CASE(NP, DMX) if (npad == NP && dm == DMX) return f(brc_kernel<NP, DMX>);
-#ifdef BRC_ONLY_64_8
-    BRC_CASE(64, 8)
-#else
-    BRC_CASE(4, 4) BRC_CASE(4, 8) BRC_CASE(4, 16)
-    BRC_CASE(8, 4) BRC_CASE(8, 8) BRC_CASE(8, 16)
-    BRC_CASE(16, 4) BRC_CASE(16, 8) BRC_CASE(16, 16)
-    BRC_CASE(32, 4) BRC_CASE(32, 8) BRC_CASE(32, 16)
-    BRC_CASE(64, 4) BRC_CASE(64, 8) BRC_CASE(64, 16)
-#endif
-#undef BRC_CASE
-    return BRC_E_INVALID;
+static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t st, const Params& P) {
+    switch (npad) {
+    case 4: return launch_step_4(dm, events, blocks, lds, st, P);
+    case 8: return launch_step_8(dm, events, blocks, lds, st, P);
+    case 16: return launch_step_16(dm, events, blocks, lds, st, P);
+    case 32: return launch_step_32(dm, events, blocks, lds, st, P);
+    case 64: return launch_step_64(dm, events, blocks, lds, st, P);
+    default: return BRC_E_INVALID;
+    }
 }
 
 static void free_all(Engine* e) {
@@ -822,12 +148,8 @@ static int clear_state(Engine* e, bool full) {
         HIPCHK(e, hipMemsetAsync(e->mgen, 0, keys * 4, e->stream));
         e->gen_budget = 0;
     } else {
-        // cells keep their generation tags; every slot keeps (and will bump) its own, so
-        // every cell written before the reset reads as stale; send steps are dropped since
-        // the step counter restarts at 0
-        const size_t m = std::max(cells, keys);
-        hipLaunchKernelGGL(reset_slots, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, e->stream, e->meta, e->mgen,
-                           (uint64_t)keys, e->cells, (uint64_t)cells);
+        hipLaunchKernelGGL(reset_slots, dim3((uint32_t)((keys + 255) / 256)), dim3(256), 0, e->stream, e->meta, e->mgen,
+                           (uint64_t)keys);
         HIPCHK(e, hipGetLastError());
     }
     HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * TS * e->nkw * 8, e->stream));
@@ -939,10 +261,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
-    const uint32_t l_words = ((uint32_t)e->dm * 64 * e->msize + 7) / 8;
-    const uint32_t h_words = (4 * 64 * e->msize + 7) / 8;
-    const uint32_t per_wave_words = e->ipw * e->NK + TS * e->nkw + 64 * e->nkw + l_words + h_words + (e->ipw * e->NK + 2) / 2 + 1;
-    e->lds_bytes = per_wave_words * 8 * WPB;
+    e->lds_bytes = lds_bytes_per_wave(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max)) * WPB;
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) { delete e; return BRC_E_INVALID; }
     auto fail = [&](int code) { free_all(e); delete e; return code; };
     if (hipSetDevice(c.device) != hipSuccess) { delete e; return BRC_E_HIP; }
@@ -1097,6 +416,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.bound_p2 = 4 * c.f;               // 2|hosts| > 4f        :88
     P.seed = c.seed; P.inst_offset = c.instance_offset; P.instances = c.instances; P.nitems = e->nitems;
     P.max_steps = max_steps ? max_steps : 0xFFFFFFFFu;
+    P.nL = delay_values(c.delay_model, c.delay_max);
     P.event_cap = c.event_capacity;
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
@@ -1105,15 +425,9 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount;
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     const uint32_t blocks = (uint32_t)((e->nitems + WPB - 1) / WPB);
-    rc = dispatch(e->npad, e->dm, [&](auto kern) {
-        if (e->lds_bytes > 64 * 1024 &&
-            hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)e->lds_bytes) != hipSuccess)
-            return (int)BRC_E_HIP;
-        kern<<<dim3(blocks), dim3(64 * WPB), e->lds_bytes, e->stream>>>(P);
-        return 0;
-    });
-    if (rc) { e->err = "no kernel instantiation"; return rc; }
-    HIPCHK(e, hipGetLastError());
+    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, blocks, e->lds_bytes, e->stream, P);
+    if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
+    if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipEventSynchronize(e->ev1));
     HIPCHK(e, hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));

@@ -1,0 +1,74 @@
+// brc_internal.h -- types shared by the engine's host code (brc_engine.hip) and the step-kernel
+// translation units (brc_kern_<NPAD>.hip).  Not part of the public ABI (include/brc.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/brc.h"
+
+namespace brc {
+
+constexpr int TS = 32;            // activity ring (steps); > max delay
+constexpr int WPB = 4;            // independent waves per workgroup
+constexpr uint32_t NEVER = 0xFFFFu;
+constexpr uint64_t TIMES_NEVER = 0xFFFFFFFF00000000ull;
+constexpr uint32_t F_EEX = 1, F_REX = 2, F_DEL = 4, F_ES = 8, F_RS = 16;
+constexpr uint32_t GEN_MASK = 0x1FFF;
+constexpr uint32_t GEN_RESTRICTED = 0x80000000u;
+constexpr uint32_t STEP_LIMIT = 60000;
+constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
+
+struct InjDev {       // 24 B, per item CSR, sorted by t
+    uint32_t t;
+    uint16_t slot, s;
+    uint8_t kind, type, seg, node;
+    int8_t value;
+    uint8_t pad[3];
+    uint64_t dst;
+};
+
+struct ItemState { uint32_t t, inj_pos, initialized, pad; };
+
+struct InstState { uint16_t status, t_stop, q_until, flags; uint32_t pad0, pad1; };
+
+struct Params {
+    uint32_t n, f, D, Q, NV, NK, nkw;
+    uint32_t protocol, delay_model, dconst, round_cap, step_cap, proposals;
+    uint32_t T_echo, T_amp, T_del, T_cnt, bound_p1, bound_p2;
+    uint64_t seed, inst_offset, instances, nitems;
+    uint32_t max_steps, nL;   // nL: delay_values() of the run
+    uint64_t event_cap;
+    uint64_t* cells;
+    uint64_t* meta; uint32_t* mgen; uint64_t* kdst;
+    uint64_t* act; uint32_t* actany; ItemState* items; InstState* inst; uint64_t* istats;
+    uint64_t* cons0; uint64_t* cons1; void* hmask;
+    const InjDev* inj; const uint32_t* inj_off; const uint32_t* inj_cnt;
+    const uint64_t* byz; const int8_t* prop;
+    brc_event* events; unsigned long long* event_count;
+    unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
+};
+
+// Distinct link delays a delay model can produce (bounds the compact delay-mask table in LDS).
+__host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) {
+    return model == BRC_DELAY_CONST ? 1u : model == BRC_DELAY_SLOWSET ? (dmax > 1 ? 2u : 1u) : dmax;
+}
+
+// Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
+// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32
+__host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL) {
+    const uint32_t ipw = 64 / (uint32_t)npad;
+    const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
+    const uint32_t h_words = (4 * 64 * msize + 7) / 8;
+    const uint32_t l_words = (nL * 64 * msize + 7) / 8;
+    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2);
+}
+
+// Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
+// Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
+int launch_step_4(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+int launch_step_8(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+int launch_step_32(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+
+}  // namespace brc

@@ -1,0 +1,9 @@
+// brc_kern_16.hip -- step-kernel instantiations for replica sets padded to NPAD = 16 lanes
+// (one translation unit per width so the build compiles them in parallel; see brc_step.h).
+#include "brc_step.h"
+
+namespace brc {
+int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+    return launch_step<16>(dm, events, blocks, lds, s, P);
+}
+}  // namespace brc

@@ -1,0 +1,9 @@
+// brc_kern_64.hip -- step-kernel instantiations for replica sets padded to NPAD = 64 lanes
+// (one translation unit per width so the build compiles them in parallel; see brc_step.h).
+#include "brc_step.h"
+
+namespace brc {
+int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+    return launch_step<64>(dm, events, blocks, lds, s, P);
+}
+}  // namespace brc

@@ -1,0 +1,724 @@
+// brc_step.h -- the MI355X (gfx950) step kernel: batched Bracha broadcast + randomized consensus.
+//
+// One 64-lane wavefront simulates an "item": IPW = 64 / NPAD independent instances, lane =
+// (instance segment, replica).  Lane d is at once receiver d (its BRB cells), sender d (its
+// send steps are read back by every receiver through __ballot) and consensus replica d.  A
+// wave runs its item from the current step to completion in ONE launch: instances are
+// independent, so no inter-wave communication exists at all.  Workgroups hold WPB such waves
+// that never synchronise with each other (LDS is partitioned per wave).
+//
+// Hot path replaced (reference = sithu/ByzantineRandomizedConsensus):
+//   brb_cell_update()  <- core/brbroadcast.py:60-119  (per-message handler, batched per step)
+//   consensus pass     <- core/byzantinerandomizedconsensus.py:53-106 (deliver / get_max_val)
+//   send_key()         <- core/byzantinerandomizedconsensus.py:43-51, base/broadcast.py:17-40
+//
+// Cell = (receiver, key).  The network suppresses duplicates (oracle/schedule.py), so every
+// ECHO/READY that reaches a cell comes from a new sender: the reference's sets
+// (core/brbroadcast.py:38-41) only ever matter through their sizes, and a cell is one word:
+//   bits  0- 4 flags  (entry in echo_sent_list, entry in ready_sent_list, delivered,
+//                      ECHO sent, READY sent)
+//   bits  5-11 |echo set|      bits 12-18 |ready set|     bits 19-31 allocation generation
+//   bits 32-47 step this lane SENT its ECHO of the key     bits 48-63 ... its READY (0xFFFF: never)
+// A cell whose generation differs from its key slot's is stale in every field, send steps
+// included, so recycling a slot (or a whole batch, brc_reset) never touches the cells.
+// HBM (lane-contiguous => every access is one coalesced 512-B wave access):
+//   cells [item][NK][64] u64
+// per instance key slots (copied to LDS for the launch): meta [inst][NK] u64 (s+1 | t_send |
+//   t_quiet | sender | value), mgen [inst][NK] u32 (generation | restricted-SEND flag),
+//   kdst [inst][NK] u64 (SEND destinations, read only for restricted SENDs)
+// per item: act [item][32][nkw] u64 (key slots that may have arrivals at step t mod 32)
+// per lane: cons0/cons1 [item][64] u64, hmask [item][4][64] T (consensus state)
+#pragma once
+#include "brc_internal.h"
+#include "schedule.h"
+
+namespace brc {
+
+#ifndef BRC_CHUNK
+#define BRC_CHUNK 4
+#endif
+constexpr int CHUNK = BRC_CHUNK;  // key slots whose cell loads are in flight together
+constexpr uint32_t NOKEY = 0xFFFFFFFFu;
+
+template <int NPAD> struct MaskOf { using type = uint64_t; };
+template <> struct MaskOf<4> { using type = uint8_t; };
+template <> struct MaskOf<8> { using type = uint8_t; };
+template <> struct MaskOf<16> { using type = uint16_t; };
+template <> struct MaskOf<32> { using type = uint32_t; };
+
+template <typename T> __device__ __forceinline__ uint32_t popc(T x) { return (uint32_t)__popcll((uint64_t)x); }
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o);
+    return x;
+}
+
+template <int NPAD> __device__ __forceinline__ uint32_t seg_max(uint32_t x) {
+#pragma unroll
+    for (int o = NPAD / 2; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+
+template <int NPAD, typename T> __device__ __forceinline__ T seg_or(T x) {
+#pragma unroll
+    for (int o = NPAD / 2; o; o >>= 1) x |= (T)__shfl_xor((unsigned long long)x, o);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t hibit(uint32_t x) { return x ? 32u - (uint32_t)__clz(x) : 0u; }
+
+// compile-time unrolled loop: f(IC<0>{}), ..., f(IC<N-1>{}) (register arrays stay statically indexed)
+template <int I> struct IC { static constexpr int value = I; };
+template <int N> struct Unrolled {
+    template <typename F> __device__ __forceinline__ static void run(F&& f) {
+        Unrolled<N - 1>::run(f);
+        f(IC<N - 1>{});
+    }
+};
+template <> struct Unrolled<0> {
+    template <typename F> __device__ __forceinline__ static void run(F&&) {}
+};
+
+// wave-uniform value -> scalar registers (valid only when every lane holds the same value)
+__device__ __forceinline__ uint32_t uni32(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    return (uint64_t)uni32((uint32_t)x) | ((uint64_t)uni32((uint32_t)(x >> 32)) << 32);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, l) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32);
+}
+
+// packed LDS/HBM key metadata
+__device__ __forceinline__ uint32_t m_s1(uint64_t m) { return (uint32_t)(m & 0xFFFF); }
+__device__ __forceinline__ uint32_t m_tsend(uint64_t m) { return (uint32_t)((m >> 16) & 0xFFFF); }
+__device__ __forceinline__ uint32_t m_tquiet(uint64_t m) { return (uint32_t)((m >> 32) & 0xFFFF); }
+__device__ __forceinline__ uint32_t m_sender(uint64_t m) { return (uint32_t)((m >> 48) & 0xFF); }
+__device__ __forceinline__ uint32_t m_value(uint64_t m) { return (uint32_t)((m >> 56) & 0xFF); }
+__device__ __forceinline__ uint64_t m_pack(uint32_t s1, uint32_t tsend, uint32_t tquiet, uint32_t sender, uint32_t value) {
+    return (uint64_t)(s1 & 0xFFFF) | ((uint64_t)(tsend & 0xFFFF) << 16) | ((uint64_t)(tquiet & 0xFFFF) << 32) |
+           ((uint64_t)(sender & 0xFF) << 48) | ((uint64_t)(value & 0xFF) << 56);
+}
+__device__ __forceinline__ uint64_t m_with_tquiet(uint64_t m, uint32_t q) {
+    return (m & ~(0xFFFFull << 32)) | ((uint64_t)(q & 0xFFFF) << 32);
+}
+
+// core/brbroadcast.py:60-119 for ONE (receiver, key) cell and every message reaching it in one
+// step, in the canonical order SEND, ECHO by sender ascending, READY by sender ascending.  All
+// arrivals grow their set (duplicates are suppressed), so the sequential threshold crossings
+// have closed forms in the set sizes:
+//   ECHO  : the first ECHO of a missing entry creates it WITHOUT the quorum check (:87-89);
+//           every later one is checked (:92-98), the last checked size is |E| after the step.
+//   READY : same creation quirk (:103-105); checked sizes run lo..hi; DELIVER at the first size
+//           >= 2f+1 (:111-115); amplification (:118-119) fires for checked sizes in [f+1, 2f]
+//           while no ECHO entry exists -- only its first firing leaves the node (duplicates).
+// Branch-free (selects only): the wave evaluates it for all 64 receivers of a key at once.
+__device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint32_t& rc, bool s_arr,
+                                                uint32_t ea, uint32_t ra, uint32_t T_echo, uint32_t T_amp,
+                                                uint32_t T_del, bool& echo_send, bool& ready_send, bool& deliver) {
+    const bool open = !(fl & F_DEL);                                        // :74
+    echo_send = open && s_arr && !(fl & F_EEX);                             // :76-82
+    fl |= echo_send ? (F_EEX | F_ES) : 0u;
+    const bool e_on = open && ea != 0;
+    const uint32_t checked = (fl & F_EEX) ? ea : ea - 1u;                   // :87-89
+    fl |= e_on ? F_EEX : 0u;
+    ec += e_on ? ea : 0u;                                                   // :89/:92
+    const bool r1 = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX); // :95-98
+    fl |= r1 ? (F_REX | F_RS) : 0u;
+    const bool r_on = open && ra != 0;
+    const bool rex = (fl & F_REX) != 0;
+    const uint32_t lo = rex ? rc + 1u : 2u, hi = rex ? rc + ra : ra;       // :103-108
+    fl |= r_on ? F_REX : 0u;
+    rc += r_on ? ra : 0u;
+    const bool any = r_on && hi >= lo;
+    const uint32_t alo = max(lo, T_amp), ahi = min(hi, T_del - 1u);
+    const bool r2 = any && !(fl & F_EEX) && alo <= ahi && !(fl & F_RS);    // :118-119
+    fl |= r2 ? F_RS : 0u;
+    deliver = any && hi >= T_del;                                           // :111-115
+    fl |= deliver ? F_DEL : 0u;
+    ready_send = r1 || r2;
+}
+
+#ifndef BRC_MIN_WAVES
+#define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
+#endif
+
+template <int NPAD, int DM, bool EV>
+__global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
+    using T = typename MaskOf<NPAD>::type;
+    constexpr int IPW = 64 / NPAD;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+
+    const int wid = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const uint64_t item = (uint64_t)blockIdx.x * WPB + wid;
+    if (item >= P.nitems) return;               // whole wave exits; waves never synchronise
+    const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
+    // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
+    //     dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32
+    const uint32_t nL = P.nL;
+    constexpr uint32_t h_words = (4 * 64 * (uint32_t)sizeof(T) + 7) / 8;
+    const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
+    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL) / 8);
+    uint64_t* s_act = s_meta + IPW * NK;
+    uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
+    T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
+    T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
+    uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
+
+    const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
+    const uint64_t inst = item * IPW + seg;
+    const bool iex = inst < P.instances;
+    const uint64_t g = P.inst_offset + inst;
+    const uint64_t all64 = (n >= 64) ? ~0ull : ((1ull << n) - 1);
+    const T allm = (T)all64;
+    const uint64_t segbits = (NPAD == 64) ? ~0ull : (((1ull << NPAD) - 1) << segbase);
+    const uint32_t mbase = seg * NK;             // this lane's instance in the LDS meta arrays
+
+    ItemState its = P.items[item];
+    uint32_t t = its.t, inj_pos = its.inj_pos;
+    const uint32_t inj_off = P.inj_off[item], inj_cnt = P.inj_cnt[item];
+    {
+        const uint64_t mb = item * IPW * (uint64_t)NK;
+        for (uint32_t i = lane; i < IPW * NK; i += 64) {
+            const bool ok = item * IPW + i / NK < P.instances;
+            s_meta[i] = ok ? P.meta[mb + i] : 0ull;
+            s_gen[i] = ok ? P.mgen[mb + i] : 0u;
+        }
+        for (uint32_t i = lane; i < TS * nkw; i += 64) s_act[i] = P.act[item * TS * nkw + i];
+        for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
+    }
+    uint32_t any_rows = uni32(P.actany[item]);   // ring rows holding any marked key (wave-uniform)
+    uint32_t lane_rows = 0;                      // rows marked by per-lane sends, merged per step
+
+    uint32_t status = BRC_DONE, t_stop = 0, q_until = 0;
+    if (iex) {
+        const uint64_t w0 = *(const uint64_t*)&P.inst[inst];     // status | t_stop | q_until | flags
+        status = w0 & 0xFFFF; t_stop = (w0 >> 16) & 0xFFFF; q_until = (w0 >> 32) & 0xFFFF;
+    }
+    const uint64_t byzm = iex ? P.byz[inst] : ~0ull;
+    const bool real = iex && (uint32_t)d < n;
+    const bool honest = real && !((byzm >> d) & 1ull);
+
+    // ---- link-delay masks: L[i] = senders j whose link j -> d has delay i+1 (schedule.h)
+    T L[DM];
+#pragma unroll
+    for (int i = 0; i < DM; ++i) L[i] = 0;
+    if (real) {
+        if (P.delay_model == BRC_DELAY_CONST) {
+#pragma unroll
+            for (int i = 0; i < DM; ++i) if ((uint32_t)i + 1 == P.dconst) L[i] = allm;
+        } else if (P.delay_model == BRC_DELAY_SLOWSET) {
+            const uint32_t off = slow_offset(P.seed, g, n);
+            T slowm = 0;
+            for (uint32_t j = 0; j < n; ++j) if (((j + n - off) % n) < P.f) slowm |= (T)((T)1 << j);
+            const bool me_slow = ((uint32_t)d + n - off) % n < P.f;
+#pragma unroll
+            for (int i = 0; i < DM; ++i) {
+                if ((uint32_t)i + 1 == D) L[i] |= me_slow ? allm : slowm;
+                if (i == 0) L[i] |= me_slow ? (T)0 : (T)(allm & ~slowm);
+            }
+        } else {
+            for (uint32_t j4 = 0; j4 < (n + 3) / 4; ++j4) {
+                const u32x4 w = draw(P.seed, g, (uint32_t)d, PURPOSE_DELAY, j4);
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t j = 4 * j4 + q;
+                    if (j >= n) break;
+                    const uint32_t dl = (P.delay_model == BRC_DELAY_UNIFORM) ? uniform_delay(ws[q], D)
+                                                                             : geometric_delay(ws[q], D);
+#pragma unroll
+                    for (int i = 0; i < DM; ++i) if ((uint32_t)i + 1 == dl) L[i] |= (T)((T)1 << j);
+                }
+            }
+        }
+    }
+    bool ovf = false, badinj = false;
+    // outset: delays (bit i <=> delay i+1) from THIS lane, as a sender, to honest receivers;
+    // outv (lane i): the senders of the wave with a delay-(i+1) link to an honest receiver
+    uint32_t outset = 0;
+    uint64_t outv = 0;
+#pragma unroll
+    for (int i = 0; i < DM; ++i) {
+        const T m = seg_or<NPAD, T>(honest ? L[i] : (T)0);
+        const bool has_i = real && ((m >> d) & 1);
+        if (has_i) outset |= 1u << i;
+        const uint64_t b = __ballot(has_i);
+        if (lane == i) outv = b;
+    }
+    const uint32_t maxout = hibit(outset);
+    const uint32_t dset = uni32(wave_or(outset));    // every delay some link of this wave has
+    // compact delay masks: the j-th delay present in the wave -> s_L[j]; every nonzero L[i] of an
+    // honest receiver is in dset (its sender's outset has bit i)
+    {
+        uint32_t j = 0;
+#pragma unroll
+        for (int i = 0; i < DM; ++i)
+            if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
+        if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
+    }
+    uint64_t* const mycells = P.cells + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
+
+    // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
+    uint64_t c0 = 0, c1 = 0;
+    const size_t li = item * 64 + lane;
+    const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
+    if (cons_lane) { c0 = P.cons0[li]; c1 = P.cons1[li]; }
+    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? ((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
+    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
+    uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
+    uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
+    uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
+
+    uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
+
+    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b) {
+        if (EV) {
+            const unsigned long long i = atomicAdd(P.event_count, 1ull);
+            if (i < P.event_cap) {
+                brc_event e;
+                e.instance = inst; e.t = t; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
+                e.type = (uint8_t)type; e.pad = 0; e.a = a; e.b = b;
+                P.events[i] = e;
+            }
+        }
+    };
+    // key k may have arrivals at t + i + 1 for every bit i of ds (called by individual lanes)
+    auto mark_lane = [&](uint32_t k, uint32_t ds) {
+        while (ds) {
+            const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
+            const uint32_t row = (t + i + 1) & (TS - 1);
+            atomicOr((unsigned long long*)&s_act[row * nkw + (k >> 6)], 1ull << (k & 63));
+            lane_rows |= 1u << row;
+        }
+    };
+    // honest origin d broadcasts SEND for its key (d, s) with value v
+    // (core/byzantinerandomizedconsensus.py:48-50 / :80-83 / :102-106, base/broadcast.py:30-35)
+    auto send_key = [&](uint32_t s, uint32_t v) {
+        const uint32_t k = (d * NV) * Q + (s % Q);
+        const uint64_t m = s_meta[mbase + k];
+        if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
+        s_gen[mbase + k] = ((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK;
+        s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
+        mark_lane(k, outset);
+        q_until = max(q_until, t + maxout);
+        st_msgs += n;
+        st_smax = max(st_smax, s);
+        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
+    };
+    auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
+        for (uint32_t i = 0; i < nvals; ++i) {
+            const uint32_t v = (order >> (2 * i)) & 3;
+            if (2 * popc(s_hm[v * 64 + lane]) > bound2) return v;
+        }
+        return 0;                                                    // str(NONE) == "-1"
+    };
+    auto cons_reset = [&]() {
+        vcount = 0; nvals = 0; order = 0;
+        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
+    };
+    auto cons_deliver = [&](uint32_t k) {                            // :53-106
+        const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = (k / Q) / NV;
+        bool found = false;
+        for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
+        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
+        s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
+        ++vcount;                                                    // :61
+        if (vcount >= P.T_cnt && phase == 1) {                       // :71
+            const uint32_t prop = get_max_val(P.bound_p1);           // :73
+            phase = 2; cons_reset();                                 // :75-78
+            send_key(2 * (round - 1) + 1, prop);                     // :80-83
+        }
+        if (vcount >= P.T_cnt && phase == 2) {                       // :86
+            const uint32_t dec = get_max_val(P.bound_p2);            // :88
+            // :89 compares str with int: never equal -> decide() always runs (:94)
+            ++dcount;
+            if (dcount == 1) { frnd = round; ft = t; fval = dec; }
+            lval = dec;
+            log_ev(BRC_EV_DECIDE, d, 0, round, dec);
+            ++round; phase = 1; cons_reset();                        // :96-100
+            send_key(2 * (round - 1), dec);                          // :102-106
+        }
+    };
+
+    // ---- actions stamped t (performed after step t's messages)
+    auto do_actions = [&]() -> bool {
+        bool mine_any = false;
+        const bool running = status == BRC_RUNNING;
+        if (its.initialized == 0 && t == 0) {
+            if (P.protocol == BRC_PROTO_CONSENSUS && P.proposals != BRC_PROPOSALS_NONE && honest && running) {
+                const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? proposal_id(P.seed, g, d)
+                                                                         : (uint32_t)P.prop[inst * n + d];
+                round = 1; phase = 1;                                 // :43-47
+                send_key(0, v & 3);
+            }
+        }
+        while (inj_pos < inj_cnt) {
+            const InjDev r = P.inj[inj_off + inj_pos];
+            if (r.t != t) break;
+            ++inj_pos;
+            const bool mine = running && seg == (int)r.seg;
+            mine_any |= mine;
+            if (r.kind == BRC_INJ_PROPOSE) {
+                if (mine && honest && d == r.node) { round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3); }
+            } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
+                // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the
+                // slot first unless that key was declared and not yet sent
+                const bool is_send = r.kind == BRC_INJ_SEND;
+                uint32_t myset = 0;
+                if (is_send && mine && honest && ((r.dst >> d) & 1ull)) {
+                    uint32_t j = 0;
+                    for (uint32_t ds = dset; ds; ds &= ds - 1, ++j)
+                        if ((s_L[j * 64 + lane] >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
+                }
+                const uint32_t os = wave_or(myset);
+                if (mine) {
+                    const uint32_t k = r.slot;
+                    if (d == 0) {
+                        uint64_t m = s_meta[mbase + k];
+                        uint32_t gen = s_gen[mbase + k] & GEN_MASK;
+                        const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
+                        if (!declared && m_s1(m) != 0 && t < m_tquiet(m)) {
+                            ovf = true;
+                        } else {
+                            uint32_t tq = m_tquiet(m);
+                            // a declared key holds its slot at least until the next step
+                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; }
+                            if (is_send) tq = max(tq, t + hibit(os));
+                            m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
+                            s_meta[mbase + k] = m;
+                            const bool restricted = is_send && (r.dst & all64) != all64;
+                            s_gen[mbase + k] = gen | (restricted ? GEN_RESTRICTED : 0u);
+                            st_smax = max(st_smax, (uint32_t)r.s);
+                            if (is_send) {
+                                P.kdst[inst * NK + k] = r.dst;
+                                mark_lane(k, os);
+                                st_msgs += __popcll(r.dst & all64);
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
+                            }
+                        }
+                    }
+                    q_until = max(q_until, t + hibit(os));
+                }
+            } else if (r.kind == BRC_INJ_MSG) {
+                const uint32_t k = r.slot;
+                bool sent = false;
+                if (mine && d == r.node) {
+                    const uint64_t m = s_meta[mbase + k];
+                    if (m_s1(m) != r.s + 1u) {
+                        badinj = true;
+                    } else {
+                        const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
+                        const size_t ci = ((size_t)item * NK + k) * 64 + lane;
+                        uint64_t wv = P.cells[ci];
+                        if (((wv >> 19) & GEN_MASK) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 19);
+                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
+                        if (!(wv & bit)) {
+                            sent = true;
+                            wv |= bit;
+                            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
+                            wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                            P.cells[ci] = wv;
+                            st_msgs += n;
+                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
+                        }
+                    }
+                }
+                const uint32_t os = wave_or(sent ? outset : 0u);
+                if (os) {
+                    if (lane == 0) mark_lane(k, os);
+                    const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
+                    if (mine && myq) {
+                        if (d == 0) {
+                            const uint64_t m = s_meta[mbase + k];
+                            if (myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
+                        }
+                        q_until = max(q_until, myq);
+                    }
+                }
+            }
+        }
+        its.initialized = 1;
+        return mine_any;
+    };
+
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (its.initialized == 0 && t == 0) {
+        do_actions();
+        q_until = seg_max<NPAD>(q_until);
+        any_rows |= uni32(wave_or(lane_rows));
+        lane_rows = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+
+    for (uint32_t it = 0; it < P.max_steps; ++it) {
+        const bool running = status == BRC_RUNNING;
+        if (!__any(running)) break;
+        // next step with possible arrivals (activity ring) or a pending action
+        const uint32_t rot = (t + 1) & (TS - 1);
+        const uint32_t rr = rot ? ((any_rows >> rot) | (any_rows << (TS - rot))) : any_rows;
+        uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
+        if (inj_pos < inj_cnt) next = min(next, P.inj[inj_off + inj_pos].t);
+        if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
+        if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
+        t = next;
+        const uint32_t row = t & (TS - 1);
+
+        // ================= BRB: the step's active key slots; one (receiver, key) cell per lane.
+        // Keys come CHUNK at a time; the next chunk's cell words are loaded while this one is
+        // processed (marks made now land on other ring rows, so the key list is fixed).
+        bool lane_active = false, any_del = false;
+        uint32_t w = 0;
+        uint64_t rem = uni64(s_act[row * nkw]);
+        auto fetch = [&](uint32_t (&kk)[CHUNK], uint64_t (&ww)[CHUNK]) {
+            Unrolled<CHUNK>::run([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                while (rem == 0 && w + 1 < nkw) { ++w; rem = uni64(s_act[row * nkw + w]); }
+                kk[c] = rem ? w * 64 + (uint32_t)(__ffsll((unsigned long long)rem) - 1) : NOKEY;
+                rem &= rem - 1;
+                ww[c] = TIMES_NEVER;
+                if (kk[c] != NOKEY) ww[c] = mycells[(size_t)kk[c] * 64];
+            });
+        };
+        auto process = [&](const uint32_t k, const uint64_t wd) {
+            uint64_t m = s_meta[mbase + k];
+            uint32_t gw = s_gen[mbase + k];
+            if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
+            const uint32_t gen = gw & GEN_MASK;
+            const bool live = running && m_s1(m) != 0;
+            const bool cur = live && real && (((uint32_t)wd >> 19) & GEN_MASK) == gen;
+            const uint64_t word = cur ? wd : TIMES_NEVER;
+            const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
+            const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
+            uint32_t ea = 0, ra = 0;
+            {
+                uint32_t j = 0;
+                for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {   // only delays some link has
+                    const uint32_t dly = (uint32_t)__ffs(ds);
+                    const uint64_t be = __ballot(dE == dly), br = __ballot(dR == dly);
+                    if (be | br) {
+                        const T Lj = s_L[j * 64 + lane];
+                        ea += popc((T)(be >> segbase) & Lj);
+                        ra += popc((T)(br >> segbase) & Lj);
+                    }
+                }
+            }
+            // SEND from the key's origin: arrives at t_send + delay(origin -> d)
+            bool s_arr = false;
+            const uint32_t dt = t - m_tsend(m);
+            const bool s_win = live && honest && dt - 1u < D;
+            if (IPW == 1 ? s_win : __any(s_win)) {
+                const uint32_t snd = m_sender(m);
+                const uint32_t bit = 1u << ((dt - 1u) & 31);
+                bool hit = false;
+                if (dset & bit) hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> snd) & 1;
+                if (hit && (gw & GEN_RESTRICTED)) hit = (P.kdst[inst * NK + k] >> d) & 1ull;
+                s_arr = s_win && hit;
+            }
+            const bool has = live && honest && (s_arr || ea || ra);
+            st_loads += (live && real) ? 1u : 0u;
+            uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
+            bool es, rs, dl;
+            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, P.T_echo, P.T_amp, P.T_del, es, rs, dl);
+            if (has) {
+                const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
+                mycells[(size_t)k * 64] = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
+                                          ((uint64_t)gen << 19) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+            }
+            st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
+            st_cells += has ? 1u : 0u;
+            st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
+            st_del += dl ? 1u : 0u;
+            lane_active |= has;
+            if (__ballot(dl)) {
+                atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
+                any_del = true;
+            }
+            if (EV) {
+                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
+                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
+                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
+            }
+            // sends: ring marks at t + every delay some sending lane has; t_quiet of the key
+            const uint64_t sb = __ballot(es || rs);
+            if (sb) {
+                uint32_t os = 0, oss = 0;
+                for (uint32_t ds = dset; ds; ds &= ds - 1) {
+                    const uint32_t i = (uint32_t)__ffs(ds) - 1;
+                    const uint64_t x = sb & readlane64(outv, (int)i);
+                    if (x) os |= 1u << i;
+                    if (IPW > 1 && ((x & segbits) != 0)) oss |= 1u << i;
+                }
+                if (IPW == 1) oss = os;
+                for (uint32_t x = os; x; x &= x - 1) {
+                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (TS - 1);
+                    if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
+                    any_rows |= 1u << r;
+                }
+                const uint32_t myq = oss ? t + hibit(oss) : 0u;
+                if (live && myq) {
+                    if (d == 0 && myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
+                    q_until = max(q_until, myq);
+                }
+            }
+        };
+        {
+            uint32_t kA[CHUNK];
+            uint64_t wA[CHUNK];
+            fetch(kA, wA);
+            while (kA[0] != NOKEY) {
+                uint32_t kB[CHUNK];
+                uint64_t wB[CHUNK];
+                fetch(kB, wB);
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    if (kA[c] != NOKEY) process(kA[c], wA[c]);
+                });
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    kA[c] = kB[c]; wA[c] = wB[c];
+                });
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+        // ================= consensus: this step's deliveries in canonical (kp, s) order
+        if (any_del) {
+            const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
+            const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
+#pragma unroll 1
+            for (uint32_t w = 0; w < nkw; ++w) {
+                uint64_t bits = s_dbits[w * 64 + lane];
+                s_dbits[w * 64 + lane] = 0;
+                if (!cons) bits = 0;
+                while (bits) {
+                    const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
+                    const uint32_t base = b0 - (b0 % Q);
+                    uint64_t grp = bits & (gm0 << base);
+                    bits &= ~(gm0 << base);
+                    while (grp) {          // several phase indices of one origin: ascending s
+                        uint32_t best = __ffsll((unsigned long long)grp) - 1;
+                        if (grp & (grp - 1)) {
+                            uint32_t bs = 0xFFFFFFFFu;
+                            for (uint64_t x = grp; x; x &= x - 1) {
+                                const uint32_t bb = __ffsll((unsigned long long)x) - 1;
+                                const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
+                                if (s1 < bs) { bs = s1; best = bb; }
+                            }
+                        }
+                        grp &= ~(1ull << best);
+                        cons_deliver(w * 64 + best);
+                    }
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+        // ================= actions stamped t
+        const bool inj_mine = do_actions();
+        any_rows |= uni32(wave_or(lane_rows));
+        lane_rows = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+        // ================= per-instance stop conditions
+        q_until = seg_max<NPAD>(q_until);
+        const uint64_t b_act = __ballot(lane_active || inj_mine) & segbits;
+        const uint64_t b_ovf = __ballot(ovf) & segbits;
+        const uint64_t b_bad = __ballot(badinj) & segbits;
+        const uint64_t b_und = __ballot(honest && dcount < P.round_cap) & segbits;
+        if (running) {
+            if (b_act) t_stop = t;
+            if (b_bad) status = BRC_BADINJ;
+            else if (b_ovf) status = BRC_OVERFLOW;
+            else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !b_und) status = BRC_DONE;
+            else if (q_until <= t) {
+                bool pending = false;
+                for (uint32_t p = inj_pos; p < inj_cnt && !pending; ++p) pending = P.inj[inj_off + p].seg == (uint32_t)seg;
+                if (!pending) status = BRC_QUIESCENT;
+            }
+        }
+        if ((uint32_t)lane < nkw) s_act[row * nkw + lane] = 0;
+        any_rows &= ~(1u << row);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+
+    // ---- write back
+    {
+        const uint64_t mb = item * IPW * (uint64_t)NK;
+        for (uint32_t i = lane; i < IPW * NK; i += 64) {
+            if (item * IPW + i / NK < P.instances) { P.meta[mb + i] = s_meta[i]; P.mgen[mb + i] = s_gen[i]; }
+        }
+        for (uint32_t i = lane; i < TS * nkw; i += 64) P.act[item * TS * nkw + i] = s_act[i];
+    }
+    if (lane == 0) {
+        P.actany[item] = any_rows;
+        ItemState o = {t, inj_pos, 1u, 0u};
+        P.items[item] = o;
+    }
+    if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
+        P.cons0[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
+                      ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        P.cons1[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
+                      ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
+        for (int v = 0; v < 4; ++v) ((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
+    }
+    // statistics: reduce over the segment, its leader writes the instance row
+    uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+        for (int o = NPAD / 2; o; o >>= 1) sums[q] += (uint32_t)__shfl_xor((int)sums[q], o);
+    }
+    if (iex && d == 0) {
+        uint64_t* ip = (uint64_t*)&P.inst[inst];
+        *ip = (*ip & 0xFFFF000000000000ull) | (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) |
+              ((uint64_t)(q_until & 0xFFFF) << 32);
+        P.istats[inst * 4 + 0] += sums[0];
+        P.istats[inst * 4 + 1] += sums[1];
+        P.istats[inst * 4 + 2] += sums[2];
+        P.istats[inst * 4 + 3] += sums[3];
+    }
+    uint64_t w6[5] = {st_cells, st_arr, st_msgs, st_del, st_loads};
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+#pragma unroll
+        for (int o = 32; o; o >>= 1) w6[q] += (uint64_t)__shfl_xor((unsigned long long)w6[q], o);
+    }
+    uint32_t smax = st_smax;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o));
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) if (w6[q]) atomicAdd(&P.gcount[q], (unsigned long long)w6[q]);
+        if (smax) atomicMax(&P.gcount[5], (unsigned long long)smax);
+    }
+}
+
+// Launch one (DM, EV) instantiation of the step kernel for a fixed NPAD.
+template <int NPAD, int DMX, bool EV>
+int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+    auto kern = brc_step<NPAD, DMX, EV>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return BRC_E_HIP;
+    kern<<<dim3(blocks), dim3(64 * WPB), lds, s>>>(P);
+    return hipGetLastError() == hipSuccess ? 0 : BRC_E_HIP;
+}
+
+template <int NPAD>
+int launch_step(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+#define BRC_CASE(DMX)                                                                         \
+    if (dm == DMX) return events ? launch_one<NPAD, DMX, true>(blocks, lds, s, P)             \
+                                 : launch_one<NPAD, DMX, false>(blocks, lds, s, P);
+#ifdef BRC_ONLY_DM8
+    BRC_CASE(8)
+#else
+    BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
+#endif
+#undef BRC_CASE
+    return BRC_E_INVALID;
+}
+
+}  // namespace brc

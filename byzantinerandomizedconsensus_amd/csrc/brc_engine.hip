@@ -93,6 +93,8 @@ struct Engine {
     uint64_t* byz = nullptr; int8_t* prop = nullptr;
     brc_event* events = nullptr; unsigned long long* event_count = nullptr;
     unsigned long long* gcount = nullptr;
+    Params* dparams = nullptr;                   // device copy of the launch parameters
+    Params hparams;
     std::vector<std::vector<InjDev>> pending;   // per item: uploaded-but-unconsumed + new
     bool inj_dirty = false, pattern_active = false;
     uint64_t gen_budget = 0;                     // generation advance bound since the last full clear
@@ -116,7 +118,7 @@ static int pick_npad(uint32_t n) {
 
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
-static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t st, const Params& P) {
+static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t st, const Params* P) {
     switch (npad) {
     case 4: return launch_step_4(dm, events, blocks, lds, st, P);
     case 8: return launch_step_8(dm, events, blocks, lds, st, P);
@@ -130,7 +132,7 @@ static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t 
 static void free_all(Engine* e) {
     void* ps[] = {e->cells, e->meta, e->mgen, e->kdst, e->act, e->actany, e->items, e->inst, e->istats,
                   e->cons0, e->cons1, e->hmask, e->inj, e->inj_off, e->inj_cnt, e->byz, e->prop, e->events,
-                  e->event_count, e->gcount};
+                  e->event_count, e->gcount, e->dparams};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -277,6 +279,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->cons0, (size_t)e->nitems * 512}, {(void**)&e->cons1, (size_t)e->nitems * 512},
         {&e->hmask, (size_t)e->nitems * 256 * e->msize}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * 8}, {(void**)&e->gcount, 64},
+        {(void**)&e->dparams, sizeof(Params)},
     };
     for (auto& a : allocs)
         if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) return fail(BRC_E_NOMEM);
@@ -423,9 +426,11 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount;
-    HIPCHK(e, hipEventRecord(e->ev0, e->stream));
     const uint32_t blocks = (uint32_t)((e->nitems + WPB - 1) / WPB);
-    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, blocks, e->lds_bytes, e->stream, P);
+    e->hparams = P;
+    HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
+    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, blocks, e->lds_bytes, e->stream, e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));

@@ -54,21 +54,22 @@ __host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) 
 }
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
-// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32
+// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32 |
+// klist[NK] u32
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = (4 * 64 * msize + 7) / 8;
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
-    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2);
+    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 1) / 2);
 }
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
-int launch_step_4(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
-int launch_step_8(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
-int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
-int launch_step_32(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
-int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P);
+int launch_step_4(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_8(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_32(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 
 }  // namespace brc

@@ -145,7 +145,11 @@ __device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint
 #endif
 
 template <int NPAD, int DM, bool EV>
-__global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
+__global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params* pp) {
+    // Parameters live in device memory, not in kernarg: the loop's global stores may alias
+    // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
+    // pinning ~60 of them in SGPRs across the hot loop.  Hot fields are copied to locals below.
+    const Params& P = *pp;
     using T = typename MaskOf<NPAD>::type;
     constexpr int IPW = 64 / NPAD;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -154,8 +158,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
     const uint64_t item = (uint64_t)blockIdx.x * WPB + wid;
     if (item >= P.nitems) return;               // whole wave exits; waves never synchronise
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
+    const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
-    //     dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32
+    //     dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK] u32
     const uint32_t nL = P.nL;
     constexpr uint32_t h_words = (4 * 64 * (uint32_t)sizeof(T) + 7) / 8;
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
@@ -165,6 +170,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
     T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
     uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
+    uint32_t* s_klist = s_gen + ((IPW * NK + 1) & ~1u); // this step's active key slots
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -453,8 +459,10 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
     }
 
     for (uint32_t it = 0; it < P.max_steps; ++it) {
-        const bool running = status == BRC_RUNNING;
-        if (!__any(running)) break;
+        const bool running0 = status == BRC_RUNNING;
+        if (!__any(running0)) break;
+        const bool running = IPW == 1 || running0;       // one instance per wave: it is running
+        const bool hon_run = honest && running, real_run = real && running;
         // next step with possible arrivals (activity ring) or a pending action
         const uint32_t rot = (t + 1) & (TS - 1);
         const uint32_t rr = rot ? ((any_rows >> rot) | (any_rows << (TS - rot))) : any_rows;
@@ -466,19 +474,23 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
         const uint32_t row = t & (TS - 1);
 
         // ================= BRB: the step's active key slots; one (receiver, key) cell per lane.
-        // Keys come CHUNK at a time; the next chunk's cell words are loaded while this one is
-        // processed (marks made now land on other ring rows, so the key list is fixed).
-        bool lane_active = false, any_del = false;
-        uint32_t w = 0;
-        uint64_t rem = uni64(s_act[row * nkw]);
-        auto fetch = [&](uint32_t (&kk)[CHUNK], uint64_t (&ww)[CHUNK]) {
+        // The ring row becomes a key list (marks made now land on other rows, so it is fixed);
+        // keys come CHUNK at a time and the next chunk's cell words load while one is processed.
+        const uint32_t cells0 = st_cells;
+        uint32_t nkeys = 0;
+        for (uint32_t w = 0; w < nkw; ++w) {
+            const uint64_t bits = uni64(s_act[row * nkw + w]);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
+            if ((bits >> lane) & 1) s_klist[nkeys + below] = w * 64 + lane;
+            nkeys += (uint32_t)__popcll(bits);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
-                while (rem == 0 && w + 1 < nkw) { ++w; rem = uni64(s_act[row * nkw + w]); }
-                kk[c] = rem ? w * 64 + (uint32_t)(__ffsll((unsigned long long)rem) - 1) : NOKEY;
-                rem &= rem - 1;
                 ww[c] = TIMES_NEVER;
-                if (kk[c] != NOKEY) ww[c] = mycells[(size_t)kk[c] * 64];
+                if (p + c < nkeys) ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * 64];
             });
         };
         auto process = [&](const uint32_t k, const uint64_t wd) {
@@ -486,8 +498,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
             uint32_t gw = s_gen[mbase + k];
             if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
             const uint32_t gen = gw & GEN_MASK;
-            const bool live = running && m_s1(m) != 0;
-            const bool cur = live && real && (((uint32_t)wd >> 19) & GEN_MASK) == gen;
+            const bool kl = m_s1(m) != 0;                        // the slot holds a key
+            const bool live = kl && running;
+            const bool cur = kl && real_run && (((uint32_t)wd >> 19) & GEN_MASK) == gen;
             const uint64_t word = cur ? wd : TIMES_NEVER;
             const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
             const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
@@ -507,34 +520,31 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
             // SEND from the key's origin: arrives at t_send + delay(origin -> d)
             bool s_arr = false;
             const uint32_t dt = t - m_tsend(m);
-            const bool s_win = live && honest && dt - 1u < D;
+            const uint32_t bit = 1u << ((dt - 1u) & 31);
+            const bool s_win = kl && dt - 1u < D && (dset & bit) != 0;     // uniform if IPW == 1
             if (IPW == 1 ? s_win : __any(s_win)) {
-                const uint32_t snd = m_sender(m);
-                const uint32_t bit = 1u << ((dt - 1u) & 31);
-                bool hit = false;
-                if (dset & bit) hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> snd) & 1;
-                if (hit && (gw & GEN_RESTRICTED)) hit = (P.kdst[inst * NK + k] >> d) & 1ull;
-                s_arr = s_win && hit;
+                bool hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> m_sender(m)) & 1;
+                if (IPW == 1 ? (gw & GEN_RESTRICTED) != 0 : __any((gw & GEN_RESTRICTED) != 0))
+                    hit = hit && ((P.kdst[inst * NK + k] >> d) & 1ull);
+                s_arr = s_win && hon_run && hit;
             }
-            const bool has = live && honest && (s_arr || ea || ra);
-            st_loads += (live && real) ? 1u : 0u;
+            const bool has = kl && hon_run && (s_arr || ea || ra);
+            st_loads += (kl && real_run) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
             bool es, rs, dl;
-            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, P.T_echo, P.T_amp, P.T_del, es, rs, dl);
-            if (has) {
+            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            {   // whole-wave store (lanes without arrivals write their word back unchanged)
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
-                mycells[(size_t)k * 64] = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
-                                          ((uint64_t)gen << 19) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+                const uint64_t nw = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
+                                    ((uint64_t)gen << 19) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+                mycells[(size_t)k * 64] = has ? nw : wd;
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;
             st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
             st_del += dl ? 1u : 0u;
-            lane_active |= has;
-            if (__ballot(dl)) {
+            if (__ballot(dl))
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
-                any_del = true;
-            }
             if (EV) {
                 const uint32_t kp = k / Q, s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
@@ -559,33 +569,31 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
                 }
                 const uint32_t myq = oss ? t + hibit(oss) : 0u;
                 if (live && myq) {
-                    if (d == 0 && myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
+                    if ((IPW == 1 || d == 0) && myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
                     q_until = max(q_until, myq);
                 }
             }
         };
         {
-            uint32_t kA[CHUNK];
             uint64_t wA[CHUNK];
-            fetch(kA, wA);
-            while (kA[0] != NOKEY) {
-                uint32_t kB[CHUNK];
+            fetch(0, wA);
+            for (uint32_t p = 0; p < nkeys; p += CHUNK) {
                 uint64_t wB[CHUNK];
-                fetch(kB, wB);
+                fetch(p + CHUNK, wB);
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    if (kA[c] != NOKEY) process(kA[c], wA[c]);
+                    if (p + c < nkeys) process(uni32(s_klist[p + c]), wA[c]);
                 });
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    kA[c] = kB[c]; wA[c] = wB[c];
+                    wA[c] = wB[c];
                 });
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
         // ================= consensus: this step's deliveries in canonical (kp, s) order
-        if (any_del) {
+        {
             const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
             const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
 #pragma unroll 1
@@ -624,7 +632,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
 
         // ================= per-instance stop conditions
         q_until = seg_max<NPAD>(q_until);
-        const uint64_t b_act = __ballot(lane_active || inj_mine) & segbits;
+        const uint64_t b_act = __ballot(st_cells != cells0 || inj_mine) & segbits;
         const uint64_t b_ovf = __ballot(ovf) & segbits;
         const uint64_t b_bad = __ballot(badinj) & segbits;
         const uint64_t b_und = __ballot(honest && dcount < P.round_cap) & segbits;
@@ -698,7 +706,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(Params P) {
 
 // Launch one (DM, EV) instantiation of the step kernel for a fixed NPAD.
 template <int NPAD, int DMX, bool EV>
-int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
     auto kern = brc_step<NPAD, DMX, EV>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -708,7 +716,7 @@ int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
 }
 
 template <int NPAD>
-int launch_step(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params& P) {
+int launch_step(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 #define BRC_CASE(DMX)                                                                         \
     if (dm == DMX) return events ? launch_one<NPAD, DMX, true>(blocks, lds, s, P)             \
                                  : launch_one<NPAD, DMX, false>(blocks, lds, s, P);

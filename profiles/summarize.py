@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise a profiles/collect.sh run into committed JSON.
 
-    python profiles/summarize.py gpurun_out/prof_<tag> profiles/<tag> [--kernel brc_kernel]
+    python profiles/summarize.py gpurun_out/prof_<tag> profiles/<tag> [--kernel brc_step]
 
 Writes <dest>/kernel_stats.csv (the rocprofv3 --stats table, copied), <dest>/pmc_summary.json
 (per-kernel mean of every PMC counter over its dispatches) and, for the headline kernel,
@@ -39,7 +39,7 @@ def kernel_avg_ns(src, kernel):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    kernel = "brc_kernel"
+    kernel = "brc_step"
     if "--kernel" in sys.argv:
         kernel = sys.argv[sys.argv.index("--kernel") + 1]
         args.remove(kernel)

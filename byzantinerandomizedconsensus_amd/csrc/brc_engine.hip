@@ -429,6 +429,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     const uint32_t blocks = (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
     rc = launch_step(e->npad, e->dm, c.event_capacity != 0, blocks, e->lds_bytes, e->stream, e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
@@ -436,16 +437,10 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
     HIPCHK(e, hipEventSynchronize(e->ev1));
     HIPCHK(e, hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
-    unsigned long long smax = 0;
-    HIPCHK(e, hipMemcpy(&smax, e->gcount + 5, 8, hipMemcpyDeviceToHost));
-    e->gen_budget += smax / c.key_window + 2;   // allocations of any one slot in this run
-    if (running_left) {
-        std::vector<InstState> ist(c.instances);
-        HIPCHK(e, hipMemcpy(ist.data(), e->inst, c.instances * sizeof(InstState), hipMemcpyDeviceToHost));
-        uint32_t r = 0;
-        for (auto& s : ist) r += s.status == BRC_RUNNING;
-        *running_left = r;
-    }
+    unsigned long long gc[8];
+    HIPCHK(e, hipMemcpy(gc, e->gcount, sizeof(gc), hipMemcpyDeviceToHost));
+    e->gen_budget += gc[5] / c.key_window + 2;   // allocations of any one slot in this run
+    if (running_left) *running_left = (uint32_t)gc[6];   // counted by the step kernel
     return BRC_OK;
 }
 

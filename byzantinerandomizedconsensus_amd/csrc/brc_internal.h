@@ -46,6 +46,7 @@ struct Params {
     const uint64_t* byz; const int8_t* prop;
     brc_event* events; unsigned long long* event_count;
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
+                                  // [6] instances still running after the launch
 };
 
 // Distinct link delays a delay model can produce (bounds the compact delay-mask table in LDS).

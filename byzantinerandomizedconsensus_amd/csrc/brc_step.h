@@ -90,6 +90,21 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l) << 32);
 }
 
+// Pointers read from device memory are generic (flat) to the compiler; flat accesses count in
+// both vmcnt and lgkmcnt, so every LDS wait would also wait for them.  gp() marks a pointer as
+// global memory (address space 1) so accesses compile to global_load/store.
+template <typename T> using gptr_t = __attribute__((address_space(1))) T*;
+template <typename T> __device__ __forceinline__ gptr_t<T> gp(T* p) { return (gptr_t<T>)p; }
+
+// one 24-B injection record through global (not flat) loads
+__device__ __forceinline__ InjDev load_inj(const InjDev* p) {
+    const gptr_t<const uint64_t> q = gp((const uint64_t*)p);
+    const uint64_t w[3] = {q[0], q[1], q[2]};
+    InjDev r;
+    __builtin_memcpy(&r, w, sizeof(r));
+    return r;
+}
+
 // packed LDS/HBM key metadata
 __device__ __forceinline__ uint32_t m_s1(uint64_t m) { return (uint32_t)(m & 0xFFFF); }
 __device__ __forceinline__ uint32_t m_tsend(uint64_t m) { return (uint32_t)((m >> 16) & 0xFFFF); }
@@ -183,26 +198,26 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
 
     ItemState its = P.items[item];
     uint32_t t = its.t, inj_pos = its.inj_pos;
-    const uint32_t inj_off = P.inj_off[item], inj_cnt = P.inj_cnt[item];
+    const uint32_t inj_off = gp(P.inj_off)[item], inj_cnt = gp(P.inj_cnt)[item];
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
             const bool ok = item * IPW + i / NK < P.instances;
-            s_meta[i] = ok ? P.meta[mb + i] : 0ull;
-            s_gen[i] = ok ? P.mgen[mb + i] : 0u;
+            s_meta[i] = ok ? gp(P.meta)[mb + i] : 0ull;
+            s_gen[i] = ok ? gp(P.mgen)[mb + i] : 0u;
         }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) s_act[i] = P.act[item * TS * nkw + i];
+        for (uint32_t i = lane; i < TS * nkw; i += 64) s_act[i] = gp(P.act)[item * TS * nkw + i];
         for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
     }
-    uint32_t any_rows = uni32(P.actany[item]);   // ring rows holding any marked key (wave-uniform)
+    uint32_t any_rows = uni32(gp(P.actany)[item]);   // ring rows holding any marked key (wave-uniform)
     uint32_t lane_rows = 0;                      // rows marked by per-lane sends, merged per step
 
     uint32_t status = BRC_DONE, t_stop = 0, q_until = 0;
     if (iex) {
-        const uint64_t w0 = *(const uint64_t*)&P.inst[inst];     // status | t_stop | q_until | flags
+        const uint64_t w0 = *(const gptr_t<uint64_t>)&gp(P.inst)[inst];     // status | t_stop | q_until | flags
         status = w0 & 0xFFFF; t_stop = (w0 >> 16) & 0xFFFF; q_until = (w0 >> 32) & 0xFFFF;
     }
-    const uint64_t byzm = iex ? P.byz[inst] : ~0ull;
+    const uint64_t byzm = iex ? gp(P.byz)[inst] : ~0ull;
     const bool real = iex && (uint32_t)d < n;
     const bool honest = real && !((byzm >> d) & 1ull);
 
@@ -264,14 +279,14 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
-    uint64_t* const mycells = P.cells + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
+    const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
     const size_t li = item * 64 + lane;
     const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
-    if (cons_lane) { c0 = P.cons0[li]; c1 = P.cons1[li]; }
-    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? ((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
+    if (cons_lane) { c0 = gp(P.cons0)[li]; c1 = gp(P.cons1)[li]; }
+    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? gp((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
     uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
     uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
@@ -355,13 +370,13 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         if (its.initialized == 0 && t == 0) {
             if (P.protocol == BRC_PROTO_CONSENSUS && P.proposals != BRC_PROPOSALS_NONE && honest && running) {
                 const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? proposal_id(P.seed, g, d)
-                                                                         : (uint32_t)P.prop[inst * n + d];
+                                                                         : (uint32_t)gp(P.prop)[inst * n + d];
                 round = 1; phase = 1;                                 // :43-47
                 send_key(0, v & 3);
             }
         }
         while (inj_pos < inj_cnt) {
-            const InjDev r = P.inj[inj_off + inj_pos];
+            const InjDev r = load_inj(P.inj + inj_off + inj_pos);
             if (r.t != t) break;
             ++inj_pos;
             const bool mine = running && seg == (int)r.seg;
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                             s_gen[mbase + k] = gen | (restricted ? GEN_RESTRICTED : 0u);
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
-                                P.kdst[inst * NK + k] = r.dst;
+                                gp(P.kdst)[inst * NK + k] = r.dst;
                                 mark_lane(k, os);
                                 st_msgs += __popcll(r.dst & all64);
                                 log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
@@ -417,7 +432,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                     } else {
                         const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
                         const size_t ci = ((size_t)item * NK + k) * 64 + lane;
-                        uint64_t wv = P.cells[ci];
+                        uint64_t wv = gp(P.cells)[ci];
                         if (((wv >> 19) & GEN_MASK) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 19);
                         const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
                         if (!(wv & bit)) {
@@ -425,7 +440,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                             wv |= bit;
                             const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            P.cells[ci] = wv;
+                            gp(P.cells)[ci] = wv;
                             st_msgs += n;
                             log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
                         }
@@ -467,7 +482,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         const uint32_t rot = (t + 1) & (TS - 1);
         const uint32_t rr = rot ? ((any_rows >> rot) | (any_rows << (TS - rot))) : any_rows;
         uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
-        if (inj_pos < inj_cnt) next = min(next, P.inj[inj_off + inj_pos].t);
+        if (inj_pos < inj_cnt) next = min(next, gp(P.inj)[inj_off + inj_pos].t);
         if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
         if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
         t = next;
@@ -525,7 +540,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             if (IPW == 1 ? s_win : __any(s_win)) {
                 bool hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> m_sender(m)) & 1;
                 if (IPW == 1 ? (gw & GEN_RESTRICTED) != 0 : __any((gw & GEN_RESTRICTED) != 0))
-                    hit = hit && ((P.kdst[inst * NK + k] >> d) & 1ull);
+                    hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = s_win && hon_run && hit;
             }
             const bool has = kl && hon_run && (s_arr || ea || ra);
@@ -643,7 +658,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !b_und) status = BRC_DONE;
             else if (q_until <= t) {
                 bool pending = false;
-                for (uint32_t p = inj_pos; p < inj_cnt && !pending; ++p) pending = P.inj[inj_off + p].seg == (uint32_t)seg;
+                for (uint32_t p = inj_pos; p < inj_cnt && !pending; ++p) pending = gp(P.inj)[inj_off + p].seg == (uint32_t)seg;
                 if (!pending) status = BRC_QUIESCENT;
             }
         }
@@ -656,21 +671,21 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            if (item * IPW + i / NK < P.instances) { P.meta[mb + i] = s_meta[i]; P.mgen[mb + i] = s_gen[i]; }
+            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i]; gp(P.mgen)[mb + i] = s_gen[i]; }
         }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) P.act[item * TS * nkw + i] = s_act[i];
+        for (uint32_t i = lane; i < TS * nkw; i += 64) gp(P.act)[item * TS * nkw + i] = s_act[i];
     }
     if (lane == 0) {
-        P.actany[item] = any_rows;
+        gp(P.actany)[item] = any_rows;
         ItemState o = {t, inj_pos, 1u, 0u};
         P.items[item] = o;
     }
     if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
-        P.cons0[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
+        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
                       ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
-        P.cons1[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
+        gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                       ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
-        for (int v = 0; v < 4; ++v) ((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
+        for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
     }
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
@@ -680,13 +695,13 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         for (int o = NPAD / 2; o; o >>= 1) sums[q] += (uint32_t)__shfl_xor((int)sums[q], o);
     }
     if (iex && d == 0) {
-        uint64_t* ip = (uint64_t*)&P.inst[inst];
+        gptr_t<uint64_t> ip = (gptr_t<uint64_t>)&gp(P.inst)[inst];
         *ip = (*ip & 0xFFFF000000000000ull) | (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) |
               ((uint64_t)(q_until & 0xFFFF) << 32);
-        P.istats[inst * 4 + 0] += sums[0];
-        P.istats[inst * 4 + 1] += sums[1];
-        P.istats[inst * 4 + 2] += sums[2];
-        P.istats[inst * 4 + 3] += sums[3];
+        gp(P.istats)[inst * 4 + 0] += sums[0];
+        gp(P.istats)[inst * 4 + 1] += sums[1];
+        gp(P.istats)[inst * 4 + 2] += sums[2];
+        gp(P.istats)[inst * 4 + 3] += sums[3];
     }
     uint64_t w6[5] = {st_cells, st_arr, st_msgs, st_del, st_loads};
 #pragma unroll
@@ -697,10 +712,12 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     uint32_t smax = st_smax;
 #pragma unroll
     for (int o = 32; o; o >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o));
+    const uint32_t nrun = popc(__ballot(iex && d == 0 && status == BRC_RUNNING));
     if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < 5; ++q) if (w6[q]) atomicAdd(&P.gcount[q], (unsigned long long)w6[q]);
         if (smax) atomicMax(&P.gcount[5], (unsigned long long)smax);
+        if (nrun) atomicAdd(&P.gcount[6], (unsigned long long)nrun);
     }
 }
 

@@ -8,6 +8,10 @@
  *   - cons_propose()        <- core/byzantinerandomizedconsensus.py:43-51
  * Dicts keyed by payload strings become a (kp, s) key table; sets of peer addresses become
  * bitsets of sender ids (sender-identity peer mode, core/brbroadcast.py:69-71).
+ * SPEC modes (see brc_oracle.h):
+ *   - brb_on_message_spec() <- Bracha's broadcast as core/brbroadcast.py:60-119 intends it
+ *   - spec_deliver()        <- core/byzantinerandomizedconsensus.py:53-106 with per-(round, phase)
+ *                              windows and the :88-92 fallback reachable (common coin)
  */
 #include "brc_oracle.h"
 #include <stdlib.h>
@@ -62,6 +66,13 @@ uint32_t oracle_proposal_id(uint64_t seed, uint64_t g, uint32_t i) {
     return 1 + (w[0] & 1u);
 }
 
+/* common coin of (instance, round): value id 1 ("0") or 2 ("1") */
+uint32_t oracle_coin_id(uint64_t coin_seed, uint64_t g, uint32_t round) {
+    uint32_t w[4];
+    draw(coin_seed, g, round, 4, 0, w);
+    return 1 + (w[0] & 1u);
+}
+
 /* ------------------------------------------------------------------ bitsets */
 typedef struct { uint64_t w[4]; } bits_t;
 static inline void bset(bits_t* b, uint32_t i) { b->w[i >> 6] |= 1ull << (i & 63); }
@@ -74,6 +85,7 @@ static inline uint32_t bcount(const bits_t* b) {
 /* ------------------------------------------------------------------ state */
 typedef struct {
     uint8_t eex, rex, del;   /* echo_sent_list / ready_sent_list entry exists, delivered */
+    uint8_t es, rs;          /* SPEC: ECHO sent, READY sent */
     bits_t e, r;             /* the two sets (core/brbroadcast.py:38-41) */
 } cell_t;
 
@@ -93,11 +105,15 @@ typedef struct {
 } bucket_t;
 
 #define NVAL 8
+#define SPEC_RING 64
 typedef struct {
     uint32_t round, phase, value_count, decides;
     uint32_t nvals;
     int32_t order[NVAL];     /* insertion order of message_values (dict order) */
     bits_t hosts[NVAL];
+    /* SPEC: deliveries buffered per phase index s (ring slot s % window) */
+    bits_t seen[SPEC_RING];
+    uint32_t cnt[SPEC_RING][2];
 } cons_t;
 
 typedef struct {
@@ -109,7 +125,7 @@ typedef struct {
     bucket_t buckets[17];
     cons_t cons[OR_MAXN];
     uint8_t delay[OR_MAXN][OR_MAXN];
-    int err;
+    int err, overflow;
 } sim_t;
 
 static uint64_t kh(uint32_t kp, uint32_t s) {
@@ -257,6 +273,93 @@ static void cons_deliver(sim_t* S, uint32_t node, int key) {
     }
 }
 
+/* ------------------------------------------------------------------ SPEC consensus */
+static uint32_t spec_window(const sim_t* S) {
+    return (S->sp->window && S->sp->window < SPEC_RING) ? S->sp->window : SPEC_RING;
+}
+
+/* Phase ends of replica `node` while its current window holds n-f distinct origins
+ * (core/byzantinerandomizedconsensus.py:71-106 as intended: thresholds of :73 and :88, the
+ * :90 "> f" fallback, and the :92 coin made common and reachable). */
+static void spec_advance(sim_t* S, uint32_t node) {
+    cons_t* c = &S->cons[node];
+    const uint32_t n = S->n, f = S->f, W = spec_window(S);
+    while (c->round > 0) {
+        const uint32_t s = 2 * (c->round - 1) + (c->phase - 1), q = s % W;
+        if (bcount(&c->seen[q]) < n - f) return;
+        const uint32_t c0 = c->cnt[q][0], c1 = c->cnt[q][1];
+        memset(&c->seen[q], 0, sizeof(bits_t));
+        c->cnt[q][0] = c->cnt[q][1] = 0;
+        if (c->phase == 1) {
+            /* :73 -- a value carried by more than (n+f)/2 of the phase's deliveries, else "-1" */
+            const int32_t prop = (2 * c0 > n + f) ? 1 : (2 * c1 > n + f) ? 2 : 0;
+            c->phase = 2;
+            cons_send_key(S, node, s + 1, prop);
+        } else {
+            /* :88-92 -- the more frequent of "0"/"1" (tie: "0"): decide above 2f, adopt above f,
+             * else the common coin of (instance, round) */
+            const int32_t vmax = (c1 > c0) ? 2 : 1;
+            const uint32_t cmax = (c1 > c0) ? c1 : c0;
+            int32_t est;
+            if (cmax > 2 * f) {
+                uint32_t ev[4] = {S->t, node, c->round, (uint32_t)vmax};
+                push_event(S->res->decide, S->res->decide_cap, &S->res->n_decide, 4, ev);
+                c->decides++;
+                est = vmax;
+            } else if (cmax > f) {
+                est = vmax;
+            } else {
+                est = (int32_t)oracle_coin_id(S->sp->coin_seed, S->sp->g, c->round);
+            }
+            c->round++;
+            c->phase = 1;
+            cons_send_key(S, node, s + 1, est);
+        }
+    }
+}
+
+/* one BRB delivery at replica `node` (SPEC): counted once per origin in the window of its
+ * phase index; earlier phases are ignored, phases beyond the window overflow */
+static void spec_deliver(sim_t* S, uint32_t node, int key) {
+    cons_t* c = &S->cons[node];
+    key_t_* k = &S->keys[key];
+    const uint32_t W = spec_window(S), host = k->kp / S->sp->nv, s = k->s;
+    const uint32_t cur = c->round ? 2 * (c->round - 1) + (c->phase - 1) : 0;
+    if (s < cur) return;
+    if (s >= cur + W) { S->overflow = 1; return; }
+    const uint32_t q = s % W;
+    if (btest(&c->seen[q], host)) return;
+    bset(&c->seen[q], host);
+    if (k->value == 1) c->cnt[q][0]++;
+    else if (k->value == 2) c->cnt[q][1]++;
+    spec_advance(S, node);
+}
+
+/* Bracha's broadcast (SPEC): ECHO on the first SEND of a key, one READY per key sent at the
+ * echo quorum or at f+1 READYs, DELIVER at 2f+1 READYs; everything after DELIVER ignored. */
+static void brb_on_message_spec(sim_t* S, const msg_t* m) {
+    key_t_* k = &S->keys[m->key];
+    cell_t* c = &k->cells[m->dst];
+    uint32_t n = S->n, f = S->f;
+    S->res->arrivals++;
+    if (c->del) return;
+    if (m->type == OR_SEND) {
+        if (!c->es) { c->es = 1; net_broadcast(S, m->dst, OR_ECHO, (int)m->key); }
+    } else if (m->type == OR_ECHO) {
+        bset(&c->e, m->src);
+        if (2u * bcount(&c->e) > n + f && !c->rs) { c->rs = 1; net_broadcast(S, m->dst, OR_READY, (int)m->key); }
+    } else if (m->type == OR_READY) {
+        bset(&c->r, m->src);
+        if (bcount(&c->r) > f && !c->rs) { c->rs = 1; net_broadcast(S, m->dst, OR_READY, (int)m->key); }
+        if (bcount(&c->r) > 2 * f) {
+            c->del = 1;
+            uint32_t ev[4] = {S->t, m->dst, k->kp, k->s};
+            push_event(S->res->deliver, S->res->deliver_cap, &S->res->n_deliver, 4, ev);
+            if (S->sp->mode == OR_MODE_SPEC) spec_deliver(S, m->dst, (int)m->key);
+        }
+    }
+}
+
 /* core/brbroadcast.py:60-119, one accept-loop iteration at node `dst`; the peer address is
  * the sender id (sender-identity mode, :71). */
 static void brb_on_message(sim_t* S, const msg_t* m) {
@@ -313,6 +416,7 @@ static void do_action(sim_t* S, const oracle_action* a) {
         cons_t* c = &S->cons[a->node];
         c->round = 1; c->phase = 1;           /* value_count is NOT reset (:44-46) */
         cons_send_key(S, a->node, 0, a->value);
+        if (S->sp->mode == OR_MODE_SPEC) spec_advance(S, a->node);   /* phase 0 may be buffered */
         break;
     }
     case OR_ACT_BRB_SEND: {                   /* BRBroadcast.broadcast(SEND, msg) */
@@ -369,10 +473,15 @@ int oracle_run(const oracle_spec* sp, oracle_result* res) {
         msg_t* v = b->v; size_t cnt = b->n;
         b->v = NULL; b->n = 0; b->cap = 0;
         qsort(v, cnt, sizeof(msg_t), msg_cmp);
-        for (size_t i = 0; i < cnt && !S->err; ++i) brb_on_message(S, &v[i]);
+        const int spec = sp->mode == OR_MODE_SPEC || sp->mode == OR_MODE_SPEC_BRB;
+        for (size_t i = 0; i < cnt && !S->err; ++i) {
+            if (spec) brb_on_message_spec(S, &v[i]);
+            else brb_on_message(S, &v[i]);
+        }
         free(v);
         while (ai < sp->n_actions && sp->actions[ai].t == nt) do_action(S, &sp->actions[ai++]);
-        if (sp->mode == OR_MODE_CONSENSUS && sp->round_cap > 0) {
+        if (S->overflow) { res->status = OR_ST_OVERFLOW; break; }
+        if ((sp->mode == OR_MODE_CONSENSUS || sp->mode == OR_MODE_SPEC) && sp->round_cap > 0) {
             int all = 1;
             for (uint32_t i = 0; i < S->n; ++i)
                 if (is_honest(S, i) && S->cons[i].decides < sp->round_cap) { all = 0; break; }

@@ -12,7 +12,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 ACT = {"propose": 1, "brb_send": 2, "byz_key": 3, "byz": 4}
-STATUS = {1: "done", 2: "quiescent", 3: "stepcap"}
+STATUS = {1: "done", 2: "quiescent", 3: "stepcap", 4: "overflow"}
+MODES = {"brb": 0, "consensus": 1, "spec": 2, "spec_brb": 3}
 
 
 class _Action(ctypes.Structure):
@@ -26,7 +27,8 @@ class _Spec(ctypes.Structure):
                 ("nv", ctypes.c_uint32), ("seed", ctypes.c_uint64), ("delay_model", ctypes.c_uint32),
                 ("dmax", ctypes.c_uint32), ("dconst", ctypes.c_uint32), ("round_cap", ctypes.c_uint32),
                 ("g", ctypes.c_uint64), ("step_cap", ctypes.c_uint32), ("n_actions", ctypes.c_uint32),
-                ("byz", ctypes.c_uint64 * 4), ("actions", ctypes.POINTER(_Action))]
+                ("byz", ctypes.c_uint64 * 4), ("actions", ctypes.POINTER(_Action)),
+                ("coin_seed", ctypes.c_uint64), ("window", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
 
 
 class _Result(ctypes.Structure):
@@ -57,6 +59,8 @@ def lib():
         L.oracle_delay.restype = ctypes.c_uint32
         L.oracle_proposal_id.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
         L.oracle_proposal_id.restype = ctypes.c_uint32
+        L.oracle_coin_id.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.oracle_coin_id.restype = ctypes.c_uint32
         L.oracle_philox.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                     ctypes.POINTER(ctypes.c_uint32)]
         L.oracle_philox.restype = None
@@ -89,11 +93,11 @@ def run(spec):
     byz = 0
     for b in spec.get("byzantine", []):
         byz |= 1 << b
-    sp = _Spec(n=spec["n"], f=spec["f"], mode=1 if spec["mode"] == "consensus" else 0,
+    sp = _Spec(n=spec["n"], f=spec["f"], mode=MODES[spec["mode"]],
                nv=spec.get("nv", 1), seed=spec["seed"], delay_model=spec["delay_model"],
                dmax=spec["dmax"], dconst=spec.get("dconst", 1), round_cap=spec.get("round_cap", 0),
                g=spec["g"], step_cap=spec.get("step_cap", 10000), n_actions=len(acts),
-               byz=_mask4(byz), actions=arr)
+               byz=_mask4(byz), actions=arr, coin_seed=spec.get("coin_seed", 0), window=spec.get("window", 0))
     cap = 4096
     while True:
         bufs = [(ctypes.c_uint32 * (cap * w))() for w in (4, 4, 5)]

@@ -10,13 +10,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
 LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK, E_INVALID, E_NOMEM, E_HIP, E_UNSUPPORTED, E_STATE = 0, -1, -2, -3, -4, -5
 ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP error",
           E_UNSUPPORTED: "unsupported workload feature", E_STATE: "invalid engine state"}
 
 PROTO_BRB, PROTO_CONSENSUS = 0, 1
+MODE_REFERENCE, MODE_SPEC = 0, 1
 PEER_SENDER = 0
 DELAY_CONST, DELAY_UNIFORM, DELAY_SLOWSET, DELAY_GEOMETRIC = 0, 1, 2, 3
 PROPOSALS_NONE, PROPOSALS_PHILOX, PROPOSALS_LOADED = 0, 1, 2
@@ -54,7 +55,8 @@ class Config(ctypes.Structure):
                 ("variants", ctypes.c_uint32), ("proposals", ctypes.c_uint32),
                 ("byz_pattern", ctypes.c_uint32), ("event_capacity", ctypes.c_uint32),
                 ("byzantine_mask", ctypes.c_uint64), ("device", ctypes.c_int32),
-                ("reserved", ctypes.c_uint32 * 7)]
+                ("mode", ctypes.c_uint32), ("coin_seed", ctypes.c_uint64),
+                ("byzantine_mask_hi", ctypes.c_uint64 * 3), ("reserved", ctypes.c_uint32 * 4)]
 
 
 class Injection(ctypes.Structure):

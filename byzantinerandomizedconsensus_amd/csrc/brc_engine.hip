@@ -78,6 +78,9 @@ __global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
 struct Engine {
     brc_config cfg;
     int npad = 0, dm = 0, ipw = 0, nkw_t = 0;
+    bool wide = false;                           // n > 64: one workgroup per instance (brc_step_wide.h)
+    uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
+    uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
     uint64_t nitems = 0;
     hipStream_t stream = nullptr;
@@ -116,6 +119,12 @@ static int pick_npad(uint32_t n) {
     return p;
 }
 
+// bits of replicas 64w .. 64w+63 that exist in an n-replica instance
+static uint64_t word_mask(uint32_t n, uint32_t w) {
+    const uint32_t lo = 64 * w;
+    return n >= lo + 64 ? ~0ull : (n <= lo ? 0ull : ((1ull << (n - lo)) - 1));
+}
+
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
 static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t st, const Params* P) {
@@ -125,6 +134,8 @@ static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t 
     case 16: return launch_step_16(dm, events, blocks, lds, st, P);
     case 32: return launch_step_32(dm, events, blocks, lds, st, P);
     case 64: return launch_step_64(dm, events, blocks, lds, st, P);
+    case 128: return launch_step_128(dm, events, blocks, lds, st, P);
+    case 256: return launch_step_256(dm, events, blocks, lds, st, P);
     default: return BRC_E_INVALID;
     }
 }
@@ -140,7 +151,7 @@ static void free_all(Engine* e) {
 }
 
 static int clear_state(Engine* e, bool full) {
-    const size_t cells = (size_t)e->nitems * e->NK * 64;
+    const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
     const size_t keys = (size_t)e->cfg.instances * e->NK;
     if (full) {
         hipLaunchKernelGGL(fill_u64, dim3((uint32_t)((cells + 255) / 256)), dim3(256), 0, e->stream, e->cells,
@@ -159,9 +170,9 @@ static int clear_state(Engine* e, bool full) {
     HIPCHK(e, hipMemsetAsync(e->items, 0, (size_t)e->nitems * sizeof(ItemState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->inst, 0, (size_t)e->cfg.instances * sizeof(InstState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->istats, 0, (size_t)e->cfg.instances * 4 * 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->cons0, 0, (size_t)e->nitems * 64 * 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->cons1, 0, (size_t)e->nitems * 64 * 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * 4 * 64 * e->msize, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->cons0, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->cons1, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * 4 * e->lpi * e->msize, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount, 0, 8 * 8, e->stream));
     if (e->event_count) HIPCHK(e, hipMemsetAsync(e->event_count, 0, 8, e->stream));
     return BRC_OK;
@@ -243,7 +254,7 @@ int brc_create(const brc_config* cfg, void** out) {
     if (!cfg || !out) return BRC_E_INVALID;
     *out = nullptr;
     const brc_config& c = *cfg;
-    if (c.n < 1 || c.n > 64 || c.instances == 0 || c.delay_max < 1 || c.delay_max > 16 ||
+    if (c.n < 1 || c.n > 256 || c.instances == 0 || c.delay_max < 1 || c.delay_max > 16 ||
         c.step_cap > STEP_LIMIT || c.peer_mode != BRC_PEER_SENDER ||
         (c.protocol != BRC_PROTO_BRB && c.protocol != BRC_PROTO_CONSENSUS) || c.delay_model > BRC_DELAY_GEOMETRIC ||
         (c.delay_model == BRC_DELAY_CONST && (c.delay_const < 1 || c.delay_const > c.delay_max)) ||
@@ -251,34 +262,40 @@ int brc_create(const brc_config* cfg, void** out) {
         !(c.variants == 1 || c.variants == 2 || c.variants == 4) || c.key_window * c.variants > 8 ||
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
-        c.proposals > BRC_PROPOSALS_LOADED)
+        c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_SPEC ||
+        (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE))
         return BRC_E_INVALID;
+    if (c.mode != BRC_MODE_REFERENCE) return BRC_E_UNSUPPORTED;
     Engine* e = new Engine();
     e->cfg = c;
     e->npad = pick_npad(c.n);
     e->dm = pick_dm(c.delay_max);
-    e->ipw = 64 / e->npad;
+    e->wide = e->npad > 64;
+    e->ipw = e->wide ? 1 : 64 / e->npad;
+    e->lpi = e->wide ? (uint32_t)e->npad : 64u;
+    e->bw = e->wide ? (uint32_t)e->npad / 64 : 1u;
     e->nkw_t = e->npad / 8 < 1 ? 1 : e->npad / 8;
     e->NK = (uint32_t)e->npad * c.variants * c.key_window;
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
-    e->lds_bytes = lds_bytes_per_wave(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max)) * WPB;
+    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max))
+                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max)) * WPB;
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) { delete e; return BRC_E_INVALID; }
     auto fail = [&](int code) { free_all(e); delete e; return code; };
     if (hipSetDevice(c.device) != hipSuccess) { delete e; return BRC_E_HIP; }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail(BRC_E_HIP);
     if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) return fail(BRC_E_HIP);
-    const size_t cells = (size_t)e->nitems * e->NK * 64;
+    const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, cells * 8}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
         {(void**)&e->kdst, keys * 8}, {(void**)&e->act, (size_t)e->nitems * TS * e->nkw * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
-        {(void**)&e->cons0, (size_t)e->nitems * 512}, {(void**)&e->cons1, (size_t)e->nitems * 512},
-        {&e->hmask, (size_t)e->nitems * 256 * e->msize}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
-        {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * 8}, {(void**)&e->gcount, 64},
+        {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},
+        {&e->hmask, (size_t)e->nitems * 4 * e->lpi * e->msize}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
+        {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
     };
     for (auto& a : allocs)
@@ -291,8 +308,11 @@ int brc_create(const brc_config* cfg, void** out) {
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->kdst, 0, keys * 8, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     {
-        std::vector<uint64_t> bm(c.instances, c.byzantine_mask & ((c.n >= 64) ? ~0ull : ((1ull << c.n) - 1)));
-        if (hipMemcpy(e->byz, bm.data(), c.instances * 8, hipMemcpyHostToDevice) != hipSuccess) return fail(BRC_E_HIP);
+        std::vector<uint64_t> bm((size_t)c.instances * e->bw);
+        for (uint64_t i = 0; i < c.instances; ++i)
+            for (uint32_t w = 0; w < e->bw; ++w)
+                bm[i * e->bw + w] = (w == 0 ? c.byzantine_mask : c.byzantine_mask_hi[w - 1]) & word_mask(c.n, w);
+        if (hipMemcpy(e->byz, bm.data(), bm.size() * 8, hipMemcpyHostToDevice) != hipSuccess) return fail(BRC_E_HIP);
     }
     if (clear_state(e, true) != BRC_OK) return fail(BRC_E_HIP);
     e->pending.assign(e->nitems, {});
@@ -318,10 +338,12 @@ int brc_load_proposals(void* h, const int8_t* proposals) {
 int brc_load_byzantine(void* h, const uint64_t* masks) {
     Engine* e = static_cast<Engine*>(h);
     if (!e || !masks) return BRC_E_INVALID;
-    const uint64_t lim = (e->cfg.n >= 64) ? ~0ull : ((1ull << e->cfg.n) - 1);
-    std::vector<uint64_t> bm(masks, masks + e->cfg.instances);
-    for (auto& m : bm) m &= lim;
-    HIPCHK(e, hipMemcpyAsync(e->byz, bm.data(), e->cfg.instances * 8, hipMemcpyHostToDevice, e->stream));
+    const uint32_t words = (e->cfg.n + 63) / 64;
+    std::vector<uint64_t> bm((size_t)e->cfg.instances * e->bw, 0);
+    for (uint64_t i = 0; i < e->cfg.instances; ++i)
+        for (uint32_t w = 0; w < words; ++w) bm[i * e->bw + w] = masks[i * words + w] & word_mask(e->cfg.n, w);
+    HIPCHK(e, hipMemcpyAsync(e->byz, bm.data(), bm.size() * 8, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     if (e->cfg.byz_pattern) { int rc = apply_pattern(e); if (rc) return rc; }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BRC_OK;
@@ -353,6 +375,10 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         } else if (x.kind == BRC_INJ_SEND || x.kind == BRC_INJ_MSG || x.kind == BRC_INJ_KEY) {
             if (x.kp >= c.n * c.variants) { e->err = "kp out of range"; return BRC_E_INVALID; }
             r.slot = (uint16_t)(x.kp * c.key_window + (x.s % c.key_window));
+            if (e->wide && x.kind != BRC_INJ_KEY && x.dst_mask != ~0ull) {
+                e->err = "n > 64: SEND / ECHO / READY injections must address every peer (dst_mask = ~0)";
+                return BRC_E_UNSUPPORTED;
+            }
             if (x.kind == BRC_INJ_MSG) {
                 if (x.type != BRC_ECHO && x.type != BRC_READY) { e->err = "MSG type must be ECHO or READY"; return BRC_E_INVALID; }
                 if ((x.dst_mask & all) != all) { e->err = "ECHO/READY injections must address every peer"; return BRC_E_UNSUPPORTED; }
@@ -426,7 +452,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount;
-    const uint32_t blocks = (uint32_t)((e->nitems + WPB - 1) / WPB);
+    const uint32_t blocks = e->wide ? (uint32_t)e->nitems : (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
@@ -448,7 +474,7 @@ int brc_reset(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return BRC_E_INVALID;
     HIPCHK(e, hipSetDevice(e->cfg.device));
-    int rc = clear_state(e, e->gen_budget >= GEN_FULL_CLEAR);
+    int rc = clear_state(e, e->gen_budget >= (e->wide ? GEN_FULL_CLEAR_W : GEN_FULL_CLEAR));
     if (rc) return rc;
     for (auto& v : e->pending) v.clear();
     e->send_keys.clear();
@@ -477,11 +503,11 @@ int brc_read_instances(void* h, uint64_t first, uint64_t count, brc_instance_res
     const uint64_t i0 = first / e->ipw, i1 = (first + count - 1) / e->ipw;
     std::vector<ItemState> its(i1 - i0 + 1);
     HIPCHK(e, hipMemcpyAsync(its.data(), e->items + i0, its.size() * sizeof(ItemState), hipMemcpyDeviceToHost, e->stream));
-    std::vector<uint64_t> c1((i1 - i0 + 1) * 64);
-    std::vector<uint64_t> bm(count);
-    HIPCHK(e, hipMemcpyAsync(bm.data(), e->byz + first, count * 8, hipMemcpyDeviceToHost, e->stream));
+    std::vector<uint64_t> c1((i1 - i0 + 1) * e->lpi);
+    std::vector<uint64_t> bm(count * e->bw);
+    HIPCHK(e, hipMemcpyAsync(bm.data(), e->byz + first * e->bw, bm.size() * 8, hipMemcpyDeviceToHost, e->stream));
     if (c.protocol == BRC_PROTO_CONSENSUS)
-        HIPCHK(e, hipMemcpyAsync(c1.data(), e->cons1 + i0 * 64, c1.size() * 8, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(c1.data(), e->cons1 + i0 * e->lpi, c1.size() * 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     for (uint64_t i = 0; i < count; ++i) {
         const uint64_t in = first + i, item = in / e->ipw, seg = in % e->ipw;
@@ -491,8 +517,8 @@ int brc_read_instances(void* h, uint64_t first, uint64_t count, brc_instance_res
         uint32_t dec = c.protocol == BRC_PROTO_CONSENSUS ? 1u : 0u;
         if (dec)
             for (uint32_t dd = 0; dd < c.n; ++dd) {
-                if ((bm[i] >> dd) & 1ull) continue;
-                if ((c1[(item - i0) * 64 + seg * e->npad + dd] & 0xFFFF) == 0) { dec = 0; break; }
+                if ((bm[i * e->bw + dd / 64] >> (dd % 64)) & 1ull) continue;
+                if ((c1[(item - i0) * e->lpi + seg * e->npad + dd] & 0xFFFF) == 0) { dec = 0; break; }
             }
         r.decided = dec;
     }
@@ -504,15 +530,15 @@ int brc_read_replicas(void* h, uint64_t first, uint64_t count, brc_replica_resul
     if (!e || !out || first + count > e->cfg.instances) return BRC_E_INVALID;
     if (!count) return BRC_OK;
     const uint64_t i0 = first / e->ipw, i1 = (first + count - 1) / e->ipw;
-    const size_t nl = (i1 - i0 + 1) * 64;
+    const size_t nl = (i1 - i0 + 1) * e->lpi;
     std::vector<uint64_t> c0(nl), c1(nl);
-    HIPCHK(e, hipMemcpyAsync(c0.data(), e->cons0 + i0 * 64, nl * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipMemcpyAsync(c1.data(), e->cons1 + i0 * 64, nl * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(c0.data(), e->cons0 + i0 * e->lpi, nl * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(c1.data(), e->cons1 + i0 * e->lpi, nl * 8, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     for (uint64_t i = 0; i < count; ++i) {
         const uint64_t in = first + i, item = in / e->ipw, seg = in % e->ipw;
         for (uint32_t dd = 0; dd < e->cfg.n; ++dd) {
-            const size_t l = (item - i0) * 64 + seg * e->npad + dd;
+            const size_t l = (item - i0) * e->lpi + seg * e->npad + dd;
             brc_replica_result& r = out[i * e->cfg.n + dd];
             const uint64_t a = c0[l], b = c1[l];
             r.round = a & 0xFFFF; r.phase = (a >> 16) & 0xFF; r.value_count = (a >> 48) & 0xFFFF;
@@ -561,14 +587,15 @@ int brc_read_stats(void* h, brc_stats* out) {
     HIPCHK(e, hipMemcpy(gc, e->gcount, 64, hipMemcpyDeviceToHost));
     out->lane_loads = gc[4];
     if (e->cfg.protocol == BRC_PROTO_CONSENSUS) {
-        std::vector<uint64_t> c1((size_t)e->nitems * 64);
-        std::vector<uint64_t> bm(N);
+        std::vector<uint64_t> c1((size_t)e->nitems * e->lpi);
+        std::vector<uint64_t> bm(N * e->bw);
         HIPCHK(e, hipMemcpy(c1.data(), e->cons1, c1.size() * 8, hipMemcpyDeviceToHost));
-        HIPCHK(e, hipMemcpy(bm.data(), e->byz, N * 8, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(bm.data(), e->byz, bm.size() * 8, hipMemcpyDeviceToHost));
         for (uint64_t in = 0; in < N; ++in) {
             const uint64_t item = in / e->ipw, seg = in % e->ipw;
             for (uint32_t dd = 0; dd < e->cfg.n; ++dd)
-                if (!((bm[in] >> dd) & 1ull)) out->decide_rounds_sum += (c1[item * 64 + seg * e->npad + dd] >> 16) & 0xFFFF;
+                if (!((bm[in * e->bw + dd / 64] >> (dd % 64)) & 1ull))
+                    out->decide_rounds_sum += (c1[item * e->lpi + seg * e->npad + dd] >> 16) & 0xFFFF;
         }
     }
     if (e->event_count) {

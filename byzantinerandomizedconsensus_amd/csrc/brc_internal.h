@@ -17,6 +17,9 @@ constexpr uint32_t GEN_MASK = 0x1FFF;
 constexpr uint32_t GEN_RESTRICTED = 0x80000000u;
 constexpr uint32_t STEP_LIMIT = 60000;
 constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
+constexpr uint32_t GEN_MASK_W = 0x7FF;      // wide kernel (n > 64): 11-bit cell generation
+constexpr uint32_t GEN_FULL_CLEAR_W = 1500;
+constexpr int CHUNK_W = 4;                  // wide kernel: keys whose ballots are exchanged per barrier
 
 struct InjDev {       // 24 B, per item CSR, sorted by t
     uint32_t t;
@@ -65,6 +68,15 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 1) / 2);
 }
 
+// Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
+// meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 | hm[4][NW][NPAD] u64 |
+// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 | klist[NK] u32 | red[12] u32
+__host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL) {
+    const uint32_t nw = (uint32_t)npad / 64;
+    return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + 4 * nw * (uint32_t)npad + 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
+           4 * (NK + NK + 12);
+}
+
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
 int launch_step_4(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
@@ -72,5 +84,8 @@ int launch_step_8(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_
 int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 int launch_step_32(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+// wide kernel (brc_step_wide.h): one workgroup of NPAD threads per instance
+int launch_step_128(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_256(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 
 }  // namespace brc

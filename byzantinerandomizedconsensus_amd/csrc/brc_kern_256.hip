@@ -1,0 +1,9 @@
+// brc_kern_256.hip -- wide step-kernel instantiations for committees padded to NPAD = 256 replicas
+// (one workgroup of 4 waves per instance; see brc_step_wide.h).
+#include "brc_step_wide.h"
+
+namespace brc {
+int launch_step_256(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    return launch_step_wide<256>(dm, events, blocks, lds, s, P);
+}
+}  // namespace brc

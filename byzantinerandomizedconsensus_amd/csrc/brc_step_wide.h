@@ -1,0 +1,665 @@
+// brc_step_wide.h -- the large-committee step kernel (gfx950): n in (64, 256], SURVEY §8(d) cfg5.
+//
+// Same protocol, same lock-step network and the same per-cell closed form as brc_step.h, but one
+// instance no longer fits a wavefront: a workgroup of NW = NPAD / 64 waves simulates ONE
+// instance, thread d = receiver d = sender d = consensus replica d.  What a 64-lane ballot did in
+// the narrow kernel becomes a per-wave ballot plus an LDS exchange:
+//   * arrivals of a key: every wave ballots "my ECHO/READY was sent `dly` steps ago" for each link
+//     delay present, lane 0 writes the word to LDS (double-buffered per chunk of keys), one
+//     workgroup barrier, then every receiver pops (ballot words & its link-delay masks);
+//   * sends: each wave marks the activity ring for its own senders (idempotent LDS atomics), the
+//     key's t_quiet is raised with a 64-bit LDS atomicMax on the packed metadata word (only that
+//     field changes in the BRB phase, so the max of the words is the max of the t_quiet fields);
+//   * per-step control (next step, status, rows of the ring) is reduced once per step through a
+//     rotating set of LDS slots (one barrier per reduction).
+// Link-delay masks do not fit LDS at n = 256 (16 delays x 256 receivers x 32 B), so each thread
+// keeps its links' delay CODES as NPL bit planes in registers (n bits per plane) and rebuilds the
+// mask of one delay with NPL ANDs per 64-bit word when a ballot word is non-zero.
+//
+// Cell word (one u64 per (receiver, key)): flags:5 | |E|:8 | |R|:8 | gen:11 | t_echo_sent:16 |
+// t_ready_sent:16.  |E| saturates at 255 (only |E| >= T_echo <= 171 is ever tested) and |R| is
+// below T_del until the cell delivers, after which it is never read (core/brbroadcast.py:74).
+//
+// Hot path replaced (reference = sithu/ByzantineRandomizedConsensus): as brc_step.h --
+//   brb_cell_update()  <- core/brbroadcast.py:60-119
+//   consensus pass     <- core/byzantinerandomizedconsensus.py:53-106
+//   send_key()         <- core/byzantinerandomizedconsensus.py:43-51, base/broadcast.py:17-40
+#pragma once
+#include "brc_step.h"
+
+namespace brc {
+
+
+__device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) x |= (uint64_t)__shfl_xor((unsigned long long)x, o);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+
+template <int NPAD, int DM, bool EV>
+__global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
+    const Params& P = *pp;
+    constexpr int NW = NPAD / 64;
+    constexpr int NPL = DM == 4 ? 2 : DM == 8 ? 3 : 4;   // bit planes of a link's delay code
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+
+    const int tid = threadIdx.x, wid = tid / 64, lane = tid % 64;
+    const uint64_t inst = blockIdx.x;
+    if (inst >= P.instances) return;            // whole workgroup exits
+    const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw, nL = P.nL;
+    const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del, model = P.delay_model;
+    // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 |
+    //   hm[4][NW][NPAD] u64 | xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
+    //   klist[NK] u32 | red[3][4] u32
+    uint64_t* s_meta = smem;
+    uint64_t* s_act = s_meta + NK;
+    uint64_t* s_dbits = s_act + TS * nkw;
+    uint64_t* s_hm = s_dbits + (size_t)nkw * NPAD;
+    uint64_t* s_xb = s_hm + 4 * NW * NPAD;
+    uint64_t* s_outm = s_xb + 2 * CHUNK_W * nL * 2 * NW;
+    uint32_t* s_gen = (uint32_t*)(s_outm + 16 * NW);
+    uint32_t* s_klist = s_gen + NK;
+    uint32_t* s_red = s_klist + NK;
+
+    const uint32_t d = (uint32_t)tid;
+    const uint64_t g = P.inst_offset + inst;
+    auto validw = [&](int w) -> uint64_t {     // senders < n in word w
+        const uint32_t lo = 64u * (uint32_t)w;
+        return n >= lo + 64 ? ~0ull : (n <= lo ? 0ull : ((1ull << (n - lo)) - 1));
+    };
+
+    ItemState its = P.items[inst];
+    uint32_t t = its.t, inj_pos = its.inj_pos;
+    const uint32_t inj_off = gp(P.inj_off)[inst], inj_cnt = gp(P.inj_cnt)[inst];
+    for (uint32_t i = d; i < NK; i += NPAD) {
+        s_meta[i] = gp(P.meta)[inst * NK + i];
+        s_gen[i] = gp(P.mgen)[inst * NK + i];
+    }
+    for (uint32_t i = d; i < TS * nkw; i += NPAD) s_act[i] = gp(P.act)[inst * TS * nkw + i];
+    for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * NPAD + d] = 0;
+    for (uint32_t i = d; i < 16 * NW; i += NPAD) s_outm[i] = 0;
+    if (d < 12) s_red[d] = 0;
+    uint32_t any_rows = uni32(gp(P.actany)[inst]);
+    uint32_t lane_rows = 0;
+
+    uint32_t status, t_stop, q_until;
+    {
+        const uint64_t w0 = *(const gptr_t<uint64_t>)&gp(P.inst)[inst];
+        status = w0 & 0xFFFF; t_stop = (w0 >> 16) & 0xFFFF; q_until = (w0 >> 32) & 0xFFFF;
+    }
+    const uint64_t byzw = gp(P.byz)[inst * NW + wid];
+    const bool real = d < n;
+    const bool honest = real && !((byzw >> lane) & 1ull);
+
+    // ---- link delays j -> d as NPL bit planes of the delay code (schedule.h)
+    uint64_t PL[NPL][NW];
+#pragma unroll
+    for (int b = 0; b < NPL; ++b)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) PL[b][w] = 0;
+    if (real) {
+        if (model == BRC_DELAY_SLOWSET) {
+            const uint32_t off = slow_offset(P.seed, g, n);
+            const bool me_slow = (d + n - off) % n < P.f;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                uint64_t sm = 0;
+                for (uint32_t b = 0; b < 64; ++b) {
+                    const uint32_t j = 64u * w + b;
+                    if (j < n && (j + n - off) % n < P.f) sm |= 1ull << b;
+                }
+                PL[0][w] = me_slow ? validw(w) : sm;          // code 1 <=> delay D
+            }
+        } else if (model == BRC_DELAY_UNIFORM || model == BRC_DELAY_GEOMETRIC) {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) {
+                for (uint32_t j4 = 0; j4 < 16; ++j4) {
+                    const uint32_t j0 = 64u * w + 4 * j4;
+                    if (j0 >= n) break;
+                    const u32x4 r = draw(P.seed, g, d, PURPOSE_DELAY, j0 >> 2);
+                    const uint32_t ws[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (j0 + q >= n) break;
+                        const uint32_t dl = (model == BRC_DELAY_UNIFORM) ? uniform_delay(ws[q], D) : geometric_delay(ws[q], D);
+#pragma unroll
+                        for (int b = 0; b < NPL; ++b)
+                            if (((dl - 1) >> b) & 1) PL[b][w] |= 1ull << (4 * j4 + q);
+                    }
+                }
+            }
+        }
+    }
+    // word w of L_dly = the senders whose link to this receiver has delay dly
+    auto Lw = [&](uint32_t dly, auto wc) -> uint64_t {
+        constexpr int w = decltype(wc)::value;
+        if (!real) return 0ull;
+        const uint64_t v = validw(w);
+        if (model == BRC_DELAY_CONST) return dly == P.dconst ? v : 0ull;
+        uint32_t code;
+        if (model == BRC_DELAY_SLOWSET) {
+            if (D == 1) return dly == 1 ? v : 0ull;
+            if (dly == D) code = 1; else if (dly == 1) code = 0; else return 0ull;
+            return code ? (v & PL[0][w]) : (v & ~PL[0][w]);
+        }
+        code = dly - 1;
+        if (code >= (1u << NPL)) return 0ull;
+        uint64_t x = v;
+#pragma unroll
+        for (int b = 0; b < NPL; ++b) x &= ((code >> b) & 1) ? PL[b][w] : ~PL[b][w];
+        return x;
+    };
+    // delay of the link o -> d (o wave-uniform)
+    auto link_delay = [&](uint32_t o) -> uint32_t {
+        if (model == BRC_DELAY_CONST) return P.dconst;
+        uint32_t code = 0;
+        const uint32_t ow = o >> 6, ob = o & 63;
+        Unrolled<NW>::run([&](auto wc) {
+            constexpr int w = decltype(wc)::value;
+            if ((uint32_t)w == ow) {
+#pragma unroll
+                for (int b = 0; b < NPL; ++b) code |= (uint32_t)((PL[b][w] >> ob) & 1ull) << b;
+            }
+        });
+        if (model == BRC_DELAY_SLOWSET) return (D > 1 && (code & 1)) ? D : 1u;
+        return code + 1;
+    };
+
+    // ---- outm[i][w]: senders with a delay-(i+1) link to some honest receiver; outset / dset
+#pragma unroll
+    for (int i = 0; i < DM; ++i) {
+        Unrolled<NW>::run([&](auto wc) {
+            constexpr int w = decltype(wc)::value;
+            const uint64_t x = wave_or64(honest ? Lw((uint32_t)i + 1, wc) : 0ull);
+            if (lane == 0 && x) atomicOr((unsigned long long*)&s_outm[i * NW + w], (unsigned long long)x);
+        });
+    }
+    __syncthreads();
+    uint32_t outset = 0, dset = 0;
+#pragma unroll
+    for (int i = 0; i < DM; ++i) {
+        uint64_t anyw = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) anyw |= s_outm[i * NW + w];
+        if (anyw) dset |= 1u << i;
+        if (real && ((s_outm[i * NW + wid] >> lane) & 1ull)) outset |= 1u << i;
+    }
+    dset = uni32(dset);
+    const uint32_t maxout = hibit(outset);
+    bool ovf = (uint32_t)__popc(dset) > nL, badinj = false;   // cannot happen: delay_values() bounds dset
+    const gptr_t<uint64_t> mycells = gp(P.cells) + inst * (uint64_t)NK * NPAD + d;   // cell (k, d) at [k * NPAD]
+
+    // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
+    uint64_t c0 = 0, c1 = 0;
+    const size_t li = inst * NPAD + d;
+    const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
+    if (cons_lane) { c0 = gp(P.cons0)[li]; c1 = gp(P.cons1)[li]; }
+    auto hm = [&](uint32_t v, uint32_t w) -> uint64_t& { return s_hm[(v * NW + w) * NPAD + d]; };
+    for (uint32_t v = 0; v < 4; ++v)
+        for (uint32_t w = 0; w < NW; ++w)
+            hm(v, w) = cons_lane ? gp((const uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] : 0ull;
+    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
+    uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
+    uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
+    uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
+
+    uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
+
+    // ---- block reductions: OR of a, OR of b, MAX of c over the workgroup (rotating LDS slots)
+    uint32_t rctr = 0;
+    auto block_red = [&](uint32_t& a, uint32_t& b, uint32_t& c) {
+        uint32_t* cur = s_red + 4 * (rctr % 3);
+        uint32_t* nxt = s_red + 4 * ((rctr + 1) % 3);
+        ++rctr;
+        const uint32_t wa = wave_or(a), wb = wave_or(b), wc = wave_max(c);
+        if (lane == 0) {
+            if (wa) atomicOr(&cur[0], wa);
+            if (wb) atomicOr(&cur[1], wb);
+            if (wc) atomicMax(&cur[2], wc);
+        }
+        if (tid == 0) { nxt[0] = 0; nxt[1] = 0; nxt[2] = 0; }
+        __syncthreads();
+        a = cur[0]; b = cur[1]; c = cur[2];
+    };
+    auto block_or = [&](uint32_t x) -> uint32_t {
+        uint32_t b = 0, c = 0;
+        block_red(x, b, c);
+        return x;
+    };
+
+    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b) {
+        if (EV) {
+            const unsigned long long i = atomicAdd(P.event_count, 1ull);
+            if (i < P.event_cap) {
+                brc_event e;
+                e.instance = inst; e.t = t; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
+                e.type = (uint8_t)type; e.pad = 0; e.a = a; e.b = b;
+                P.events[i] = e;
+            }
+        }
+    };
+    auto mark_lane = [&](uint32_t k, uint32_t ds) {
+        while (ds) {
+            const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
+            const uint32_t row = (t + i + 1) & (TS - 1);
+            atomicOr((unsigned long long*)&s_act[row * nkw + (k >> 6)], 1ull << (k & 63));
+            lane_rows |= 1u << row;
+        }
+    };
+    auto send_key = [&](uint32_t s, uint32_t v) {
+        const uint32_t k = (d * NV) * Q + (s % Q);
+        const uint64_t m = s_meta[k];
+        if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
+        s_gen[k] = ((s_gen[k] & GEN_MASK_W) + 1) & GEN_MASK_W;
+        s_meta[k] = m_pack(s + 1, t, t + maxout, d, v);
+        mark_lane(k, outset);
+        q_until = max(q_until, t + maxout);
+        st_msgs += n;
+        st_smax = max(st_smax, s);
+        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
+    };
+    auto popc_hm = [&](uint32_t v) -> uint32_t {
+        uint32_t c = 0;
+        for (uint32_t w = 0; w < NW; ++w) c += (uint32_t)__popcll(hm(v, w));
+        return c;
+    };
+    auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
+        for (uint32_t i = 0; i < nvals; ++i) {
+            const uint32_t v = (order >> (2 * i)) & 3;
+            if (2 * popc_hm(v) > bound2) return v;
+        }
+        return 0;                                                    // str(NONE) == "-1"
+    };
+    auto cons_reset = [&]() {
+        vcount = 0; nvals = 0; order = 0;
+        for (uint32_t v = 0; v < 4; ++v)
+            for (uint32_t w = 0; w < NW; ++w) hm(v, w) = 0;
+    };
+    auto cons_deliver = [&](uint32_t k) {                            // :53-106
+        const uint32_t v = m_value(s_meta[k]) & 3, host = (k / Q) / NV;
+        bool found = false;
+        for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
+        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
+        hm(v, host >> 6) |= 1ull << (host & 63);                     // :60
+        ++vcount;                                                    // :61
+        if (vcount >= P.T_cnt && phase == 1) {                       // :71
+            const uint32_t prop = get_max_val(P.bound_p1);           // :73
+            phase = 2; cons_reset();                                 // :75-78
+            send_key(2 * (round - 1) + 1, prop);                     // :80-83
+        }
+        if (vcount >= P.T_cnt && phase == 2) {                       // :86
+            const uint32_t dec = get_max_val(P.bound_p2);            // :88
+            ++dcount;                                                // :89 never equal -> :94
+            if (dcount == 1) { frnd = round; ft = t; fval = dec; }
+            lval = dec;
+            log_ev(BRC_EV_DECIDE, d, 0, round, dec);
+            ++round; phase = 1; cons_reset();                        // :96-100
+            send_key(2 * (round - 1), dec);                          // :102-106
+        }
+    };
+
+    // ---- actions stamped t (performed after step t's messages); every branch is workgroup-uniform
+    auto do_actions = [&]() -> bool {
+        bool mine_any = false;
+        const bool running = status == BRC_RUNNING;
+        if (its.initialized == 0 && t == 0) {
+            if (P.protocol == BRC_PROTO_CONSENSUS && P.proposals != BRC_PROPOSALS_NONE && honest && running) {
+                const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? proposal_id(P.seed, g, d)
+                                                                         : (uint32_t)gp(P.prop)[inst * n + d];
+                round = 1; phase = 1;                                 // :43-47
+                send_key(0, v & 3);
+            }
+        }
+        while (inj_pos < inj_cnt) {
+            const InjDev r = load_inj(P.inj + inj_off + inj_pos);
+            if (r.t != t) break;
+            ++inj_pos;
+            const bool mine = running;
+            mine_any |= mine;
+            if (r.kind == BRC_INJ_PROPOSE) {
+                if (mine && honest && d == r.node) { round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3); }
+            } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
+                // every peer is a destination (brc_inject rejects restricted SENDs for n > 64)
+                const bool is_send = r.kind == BRC_INJ_SEND;
+                uint32_t myset = 0;
+                if (is_send && mine && honest) myset = 1u << (link_delay(r.node) - 1);
+                const uint32_t os = block_or(myset);
+                if (mine) {
+                    const uint32_t k = r.slot;
+                    if (d == 0) {
+                        uint64_t m = s_meta[k];
+                        uint32_t gen = s_gen[k] & GEN_MASK_W;
+                        const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
+                        if (!declared && m_s1(m) != 0 && t < m_tquiet(m)) {
+                            ovf = true;
+                        } else {
+                            uint32_t tq = m_tquiet(m);
+                            if (!declared) { gen = (gen + 1) & GEN_MASK_W; tq = t + 1; }
+                            if (is_send) tq = max(tq, t + hibit(os));
+                            m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
+                            s_meta[k] = m;
+                            s_gen[k] = gen;
+                            st_smax = max(st_smax, (uint32_t)r.s);
+                            if (is_send) {
+                                mark_lane(k, os);
+                                st_msgs += n;
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
+                            }
+                        }
+                    }
+                    q_until = max(q_until, t + hibit(os));
+                }
+            } else if (r.kind == BRC_INJ_MSG) {
+                const uint32_t k = r.slot;
+                bool sent = false;
+                if (mine && d == r.node) {
+                    const uint64_t m = s_meta[k];
+                    if (m_s1(m) != r.s + 1u) {
+                        badinj = true;
+                    } else {
+                        const uint32_t gen = s_gen[k] & GEN_MASK_W;
+                        uint64_t wv = mycells[(size_t)k * NPAD];
+                        if (((wv >> 21) & GEN_MASK_W) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 21);
+                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
+                        if (!(wv & bit)) {
+                            sent = true;
+                            wv |= bit;
+                            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
+                            wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                            mycells[(size_t)k * NPAD] = wv;
+                            st_msgs += n;
+                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
+                        }
+                    }
+                }
+                const uint32_t os = block_or(sent ? outset : 0u);
+                if (os) {
+                    if (d == 0) mark_lane(k, os);
+                    const uint32_t myq = t + hibit(os);
+                    if (mine) {
+                        if (d == 0 && myq > m_tquiet(s_meta[k])) s_meta[k] = m_with_tquiet(s_meta[k], myq);
+                        q_until = max(q_until, myq);
+                    }
+                }
+            }
+        }
+        its.initialized = 1;
+        return mine_any;
+    };
+
+    __syncthreads();
+    if (its.initialized == 0 && t == 0) {
+        do_actions();
+        uint32_t a = 0;
+        block_red(a, lane_rows, q_until);
+        any_rows |= lane_rows;
+        lane_rows = 0;
+    }
+
+    for (uint32_t it = 0; it < P.max_steps; ++it) {
+        if (status != BRC_RUNNING) break;                 // workgroup-uniform
+        const uint32_t rot = (t + 1) & (TS - 1);
+        const uint32_t rr = rot ? ((any_rows >> rot) | (any_rows << (TS - rot))) : any_rows;
+        uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
+        if (inj_pos < inj_cnt) next = min(next, gp(P.inj)[inj_off + inj_pos].t);
+        if (next == 0xFFFFFFFFu) { status = BRC_QUIESCENT; break; }
+        if (next > P.step_cap) { status = BRC_STEPCAP; break; }
+        t = next;
+        const uint32_t row = t & (TS - 1);
+
+        // ================= BRB: this step's active key slots
+        const uint32_t cells0 = st_cells;
+        uint32_t nkeys = 0;
+        for (uint32_t w = 0; w < nkw; ++w) {
+            const uint64_t bits = uni64(s_act[row * nkw + w]);
+            if (wid == 0) {
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
+                if ((bits >> lane) & 1) s_klist[nkeys + below] = w * 64 + lane;
+            }
+            nkeys += (uint32_t)__popcll(bits);
+        }
+        __syncthreads();
+
+        // phase 1 of a chunk: ballot words "my ECHO / READY of key c was sent dly steps ago"
+        auto ballots = [&](uint32_t p, uint32_t buf, const uint64_t (&ww)[CHUNK_W]) {
+            Unrolled<CHUNK_W>::run([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                if (p + c < nkeys) {
+                    const uint32_t k = uni32(s_klist[p + c]);
+                    const uint64_t m = uni64(s_meta[k]);
+                    const uint32_t gen = uni32(s_gen[k]) & GEN_MASK_W;
+                    const bool cur = m_s1(m) != 0 && real && (((uint32_t)ww[c] >> 21) & GEN_MASK_W) == gen;
+                    const uint64_t word = cur ? ww[c] : TIMES_NEVER;
+                    const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
+                    uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
+                    uint32_t j = 0;
+                    for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
+                        const uint32_t dly = (uint32_t)__ffs(ds);
+                        const uint64_t be = __ballot(dE == dly), br = __ballot(dR == dly);
+                        if (lane == 0) { xb[j * 2 * NW + wid] = be; xb[j * 2 * NW + NW + wid] = br; }
+                    }
+                }
+            });
+        };
+        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK_W]) {
+            Unrolled<CHUNK_W>::run([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                ww[c] = TIMES_NEVER;
+                if (p + c < nkeys) ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * NPAD];
+            });
+        };
+        // phase 2: one (receiver d, key k) cell
+        auto process = [&](const uint32_t k, const uint64_t wd, uint32_t buf, int c) {
+            const uint64_t m = uni64(s_meta[k]);
+            const uint32_t gw = uni32(s_gen[k]);
+            const uint32_t gen = gw & GEN_MASK_W;
+            const bool kl = m_s1(m) != 0;                        // the slot holds a key
+            const bool cur = kl && real && (((uint32_t)wd >> 21) & GEN_MASK_W) == gen;
+            const uint64_t word = cur ? wd : TIMES_NEVER;
+            const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
+            uint32_t ea = 0, ra = 0;
+            {
+                const uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
+                uint32_t j = 0;
+                for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
+                    const uint32_t dly = (uint32_t)__ffs(ds);
+                    uint64_t xe[NW], xr[NW], any = 0;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) { xe[w] = xb[j * 2 * NW + w]; xr[w] = xb[j * 2 * NW + NW + w]; any |= xe[w] | xr[w]; }
+                    if (any) {
+                        Unrolled<NW>::run([&](auto wc) {
+                            constexpr int w = decltype(wc)::value;
+                            const uint64_t L = Lw(dly, wc);
+                            ea += (uint32_t)__popcll(xe[w] & L);
+                            ra += (uint32_t)__popcll(xr[w] & L);
+                        });
+                    }
+                }
+            }
+            // SEND from the key's origin: arrives at t_send + delay(origin -> d)
+            bool s_arr = false;
+            const uint32_t dt = t - m_tsend(m);
+            const bool s_win = kl && dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);   // uniform
+            if (s_win) s_arr = honest && link_delay(m_sender(m)) == dt;
+            const bool has = kl && honest && (s_arr || ea || ra);
+            st_loads += (kl && real) ? 1u : 0u;
+            uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 255, rc = (uint32_t)(word >> 13) & 255;
+            bool es, rs, dl;
+            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            {
+                const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
+                const uint64_t nw = (uint64_t)fl | ((uint64_t)min(ec, 255u) << 5) | ((uint64_t)min(rc, 255u) << 13) |
+                                    ((uint64_t)gen << 21) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+                mycells[(size_t)k * NPAD] = has ? nw : wd;
+            }
+            st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
+            st_cells += has ? 1u : 0u;
+            st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
+            st_del += dl ? 1u : 0u;
+            if (dl) s_dbits[(k >> 6) * NPAD + d] |= 1ull << (k & 63);
+            if (EV) {
+                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
+                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
+                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
+            }
+            // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
+            const uint64_t sb = __ballot(es || rs);
+            if (sb) {
+                uint32_t os = 0;
+                for (uint32_t ds = dset; ds; ds &= ds - 1) {
+                    const uint32_t i = (uint32_t)__ffs(ds) - 1;
+                    if (sb & s_outm[i * NW + wid]) os |= 1u << i;
+                }
+                for (uint32_t x = os; x; x &= x - 1) {
+                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (TS - 1);
+                    if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
+                    lane_rows |= 1u << r;
+                }
+                if (kl && os) {
+                    const uint32_t myq = t + hibit(os);
+                    if (lane == 0) atomicMax((unsigned long long*)&s_meta[k], (unsigned long long)m_with_tquiet(m, myq));
+                    q_until = max(q_until, myq);
+                }
+            }
+        };
+        {
+            uint64_t wA[CHUNK_W];
+            fetch(0, wA);
+            for (uint32_t p = 0; p < nkeys; p += CHUNK_W) {
+                const uint32_t buf = (p / CHUNK_W) & 1;
+                ballots(p, buf, wA);
+                __syncthreads();
+                uint64_t wB[CHUNK_W];
+                fetch(p + CHUNK_W, wB);
+                Unrolled<CHUNK_W>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    if (p + c < nkeys) process(uni32(s_klist[p + c]), wA[c], buf, c);
+                });
+                Unrolled<CHUNK_W>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    wA[c] = wB[c];
+                });
+            }
+        }
+        __syncthreads();
+
+        // ================= consensus: this step's deliveries in canonical (kp, s) order
+        {
+            const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
+            const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest;
+#pragma unroll 1
+            for (uint32_t w = 0; w < nkw; ++w) {
+                uint64_t bits = s_dbits[w * NPAD + d];
+                s_dbits[w * NPAD + d] = 0;
+                if (!cons) bits = 0;
+                while (bits) {
+                    const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
+                    const uint32_t base = b0 - (b0 % Q);
+                    uint64_t grp = bits & (gm0 << base);
+                    bits &= ~(gm0 << base);
+                    while (grp) {          // several phase indices of one origin: ascending s
+                        uint32_t best = __ffsll((unsigned long long)grp) - 1;
+                        if (grp & (grp - 1)) {
+                            uint32_t bs = 0xFFFFFFFFu;
+                            for (uint64_t x = grp; x; x &= x - 1) {
+                                const uint32_t bb = __ffsll((unsigned long long)x) - 1;
+                                const uint32_t s1 = m_s1(s_meta[w * 64 + bb]);
+                                if (s1 < bs) { bs = s1; best = bb; }
+                            }
+                        }
+                        grp &= ~(1ull << best);
+                        cons_deliver(w * 64 + best);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+
+        // ================= actions stamped t
+        const bool inj_mine = do_actions();
+
+        // ================= per-instance stop conditions (one workgroup reduction)
+        uint32_t flags = ((st_cells != cells0 || inj_mine) ? 1u : 0u) | (ovf ? 2u : 0u) | (badinj ? 4u : 0u) |
+                         ((honest && dcount < P.round_cap) ? 8u : 0u);
+        block_red(flags, lane_rows, q_until);
+        any_rows |= lane_rows;
+        lane_rows = 0;
+        if (flags & 1u) t_stop = t;
+        if (flags & 4u) status = BRC_BADINJ;
+        else if (flags & 2u) status = BRC_OVERFLOW;
+        else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !(flags & 8u)) status = BRC_DONE;
+        else if (q_until <= t && inj_pos >= inj_cnt) status = BRC_QUIESCENT;
+        if (d < nkw) s_act[row * nkw + d] = 0;
+        any_rows &= ~(1u << row);
+    }
+    __syncthreads();
+
+    // ---- write back
+    for (uint32_t i = d; i < NK; i += NPAD) { gp(P.meta)[inst * NK + i] = s_meta[i]; gp(P.mgen)[inst * NK + i] = s_gen[i]; }
+    for (uint32_t i = d; i < TS * nkw; i += NPAD) gp(P.act)[inst * TS * nkw + i] = s_act[i];
+    if (d == 0) {
+        gp(P.actany)[inst] = any_rows;
+        ItemState o = {t, inj_pos, 1u, 0u};
+        P.items[inst] = o;
+    }
+    if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
+        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
+                          ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
+                          ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
+        for (uint32_t v = 0; v < 4; ++v)
+            for (uint32_t w = 0; w < NW; ++w) gp((uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] = hm(v, w);
+    }
+    // statistics: wave sums, then one atomic per wave and counter
+    uint64_t w6[5] = {st_cells, st_arr, st_msgs, st_del, st_loads};
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+#pragma unroll
+        for (int o = 32; o; o >>= 1) w6[q] += (uint64_t)__shfl_xor((unsigned long long)w6[q], o);
+    }
+    const uint32_t smax = wave_max(st_smax);
+    if (lane == 0) {
+        // istats row: msgs, arrivals, cell-steps, deliveries
+        const uint64_t row4[4] = {w6[2], w6[1], w6[0], w6[3]};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) if (row4[q]) atomicAdd((unsigned long long*)&P.istats[inst * 4 + q], (unsigned long long)row4[q]);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) if (w6[q]) atomicAdd(&P.gcount[q], (unsigned long long)w6[q]);
+        if (smax) atomicMax(&P.gcount[5], (unsigned long long)smax);
+    }
+    if (d == 0) {
+        gptr_t<uint64_t> ip = (gptr_t<uint64_t>)&gp(P.inst)[inst];
+        *ip = (*ip & 0xFFFF000000000000ull) | (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) |
+              ((uint64_t)(q_until & 0xFFFF) << 32);
+        if (status == BRC_RUNNING) atomicAdd(&P.gcount[6], 1ull);
+    }
+}
+
+template <int NPAD, int DMX, bool EV>
+int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    auto kern = brc_step_wide<NPAD, DMX, EV>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return BRC_E_HIP;
+    kern<<<dim3(blocks), dim3(NPAD), lds, s>>>(P);
+    return hipGetLastError() == hipSuccess ? 0 : BRC_E_HIP;
+}
+
+template <int NPAD>
+int launch_step_wide(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+#define BRC_CASE(DMX)                                                                         \
+    if (dm == DMX) return events ? launch_wide_one<NPAD, DMX, true>(blocks, lds, s, P)        \
+                                 : launch_wide_one<NPAD, DMX, false>(blocks, lds, s, P);
+    BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
+#undef BRC_CASE
+    return BRC_E_INVALID;
+}
+
+}  // namespace brc

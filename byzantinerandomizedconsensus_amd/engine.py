@@ -9,6 +9,8 @@ import numpy as np
 
 from . import _lib as L
 
+M64 = (1 << 64) - 1
+
 
 def _check(lib, handle, rc):
     if rc != L.OK:
@@ -25,7 +27,7 @@ class Engine:
     def __init__(self, n, f, instances, protocol="consensus", seed=0, delay_model=L.DELAY_CONST,
                  delay_max=1, delay_const=1, round_cap=1, step_cap=4000, key_window=4, variants=1,
                  proposals=L.PROPOSALS_NONE, byz_pattern=L.BYZ_NONE, byzantine=(), event_capacity=0,
-                 instance_offset=0, device=0):
+                 instance_offset=0, device=0, mode=L.MODE_REFERENCE, coin_seed=0):
         self._lib = L.load()
         self._h = ctypes.c_void_p()
         mask = 0
@@ -37,7 +39,9 @@ class Engine:
                             delay_max=delay_max, delay_const=delay_const, round_cap=round_cap,
                             step_cap=step_cap, key_window=key_window, variants=variants,
                             proposals=proposals, byz_pattern=byz_pattern, event_capacity=event_capacity,
-                            byzantine_mask=mask, device=device)
+                            byzantine_mask=mask & M64, device=device, mode=mode, coin_seed=coin_seed)
+        for w in range(3):
+            self.cfg.byzantine_mask_hi[w] = (mask >> (64 * (w + 1))) & M64
         rc = self._lib.brc_create(ctypes.byref(self.cfg), ctypes.byref(self._h))
         if rc != L.OK:
             raise L.EngineError(rc, "brc_create rejected the configuration")
@@ -70,7 +74,9 @@ class Engine:
         self._chk(self._lib.brc_load_proposals(self._h, arr.ctypes.data_as(ctypes.c_void_p)))
 
     def load_byzantine(self, masks):
-        arr = np.ascontiguousarray(masks, dtype=np.uint64).reshape(self.instances)
+        """masks: [instances] (n <= 64) or [instances][(n + 63) // 64] uint64 words (bit d of word
+        w = replica 64 w + d is Byzantine)."""
+        arr = np.ascontiguousarray(masks, dtype=np.uint64).reshape(self.instances, (self.n + 63) // 64)
         self._chk(self._lib.brc_load_byzantine(self._h, arr.ctypes.data_as(ctypes.c_void_p)))
 
     def inject(self, items):
@@ -89,7 +95,9 @@ class Engine:
             a.kp = x.get("kp", 0)
             a.s = x.get("s", 0)
             a.value = x.get("value", 0)
-            a.dst_mask = x.get("dst", 0) & 0xFFFFFFFFFFFFFFFF
+            dst = x.get("dst", 0)
+            # n > 64: the engine takes only "every peer" destinations, spelled ~0
+            a.dst_mask = M64 if (self.n > 64 and dst == (1 << self.n) - 1) else dst & M64
         self._chk(self._lib.brc_inject(self._h, arr, len(items)))
 
     # ------------------------------------------------------------------ execution

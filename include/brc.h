@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 1
+#define BRC_ABI_VERSION 2
 
 enum {
     BRC_OK = 0,
@@ -45,6 +45,11 @@ enum {
 };
 
 enum { BRC_PROTO_BRB = 0, BRC_PROTO_CONSENSUS = 1 };
+/* BRC_MODE_REFERENCE: the protocol exactly as the reference runs it, quirks included (SURVEY §4
+ * K1-K12).  BRC_MODE_SPEC: the protocol the reference intends (Bracha-correct broadcast; consensus
+ * with per-phase windows and the core/byzantinerandomizedconsensus.py:88-92 coin made reachable as
+ * a common Philox coin keyed (coin_seed, instance, round)). */
+enum { BRC_MODE_REFERENCE = 0, BRC_MODE_SPEC = 1 };
 enum { BRC_PEER_SENDER = 0 };
 enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DELAY_GEOMETRIC = 3 };
 enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };
@@ -55,7 +60,7 @@ enum { BRC_RUNNING = 0, BRC_DONE = 1, BRC_QUIESCENT = 2, BRC_STEPCAP = 3, BRC_OV
 enum { BRC_EV_DELIVER = 1, BRC_EV_DECIDE = 2, BRC_EV_SEND = 3 };
 
 typedef struct {
-    uint32_t n;               /* replicas per instance, self included (1..64) */
+    uint32_t n;               /* replicas per instance, self included (1..256) */
     uint32_t f;               /* fault bound: thresholds (n+f)/2, f+1, 2f+1, n-f+1 */
     uint32_t protocol;        /* BRC_PROTO_* */
     uint32_t peer_mode;       /* BRC_PEER_SENDER (core/brbroadcast.py:71 identity) */
@@ -72,9 +77,12 @@ typedef struct {
     uint32_t proposals;       /* BRC_PROPOSALS_* (consensus) */
     uint32_t byz_pattern;     /* BRC_BYZ_* applied to every instance */
     uint32_t event_capacity;  /* 0: no event log */
-    uint64_t byzantine_mask;  /* replicas that run no code (all instances; see brc_load_byzantine) */
+    uint64_t byzantine_mask;  /* replicas 0..63 that run no code (all instances; see brc_load_byzantine) */
     int32_t device;           /* HIP device ordinal */
-    uint32_t reserved[7];
+    uint32_t mode;            /* BRC_MODE_* */
+    uint64_t coin_seed;       /* BRC_MODE_SPEC: common-coin key */
+    uint64_t byzantine_mask_hi[3];  /* replicas 64..255 that run no code */
+    uint32_t reserved[4];
 } brc_config;
 
 typedef struct {
@@ -86,7 +94,8 @@ typedef struct {
     uint32_t kp;              /* key slot: origin * variants + variant */
     uint32_t s;               /* phase index 2*(round-1)+(phase-1), or BRB sequence */
     int32_t value;            /* value id (0 == "-1") */
-    uint64_t dst_mask;        /* BRC_INJ_SEND destinations; BRC_INJ_MSG must be all peers */
+    uint64_t dst_mask;        /* BRC_INJ_SEND destinations; BRC_INJ_MSG must be all peers.
+                                 n > 64: both must be ~0 (every peer) */
 } brc_injection;
 
 typedef struct {
@@ -124,7 +133,7 @@ typedef struct {
 
 int brc_create(const brc_config* cfg, void** engine);
 int brc_load_proposals(void* engine, const int8_t* proposals /* [instances][n] value ids */);
-int brc_load_byzantine(void* engine, const uint64_t* byz_masks /* [instances] */);
+int brc_load_byzantine(void* engine, const uint64_t* byz_masks /* [instances][(n + 63) / 64] */);
 int brc_inject(void* engine, const brc_injection* list, size_t count);
 int brc_run(void* engine, uint32_t max_steps, uint32_t* running_left);
 int brc_reset(void* engine);

@@ -194,6 +194,13 @@ def scenario_groups():
                                 for (m, d) in ((1, 4), (2, 4), (0, 1)) for g in range(2)]
     G["cons_slowset_n16"] = [cons_spec(16, 5, 0x5EED0004, 2, 8, g, round_cap=2) for g in range(3)]
     G["cons_slowset_n64"] = [cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1) for g in range(1)]
+    # large committees (the wide kernel, n > 64)
+    G["brb_uniform_n100"] = [brb_spec(100, 33, 0x5EED0005, 1, 4, g, [(0, 0, 0), (0, 57, 0), (3, 99, 0), (5, 0, 1)])
+                             for g in range(2)]
+    G["brb_geometric_n256"] = [brb_spec(256, 85, 0x5EED0005, 3, 16, g, [(0, 7, 0), (2, 200, 0)]) for g in range(1)]
+    G["brb_slowset_n256"] = [brb_spec(256, 85, 0x5EED0005, 2, 8, g, [(0, 130, 0)]) for g in range(1)]
+    G["cons_uniform_n70"] = [cons_spec(70, 23, 0x5EED0005, 1, 4, g, round_cap=1) for g in range(1)]
+    G["cons_slowset_n70"] = [cons_spec(70, 23, 0x5EED0005, 2, 8, g, round_cap=1) for g in range(1)]
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))

@@ -35,7 +35,7 @@ def test_invalid_config_rejected_without_gpu():
     h = ctypes.c_void_p()
     bad = L.Config(n=0, f=0, instances=1, delay_max=1, delay_const=1, key_window=4, variants=1)
     assert lib.brc_create(ctypes.byref(bad), ctypes.byref(h)) == L.E_INVALID
-    bad = L.Config(n=65, f=0, instances=1, delay_max=1, delay_const=1, key_window=4, variants=1)
+    bad = L.Config(n=257, f=0, instances=1, delay_max=1, delay_const=1, key_window=4, variants=1)
     assert lib.brc_create(ctypes.byref(bad), ctypes.byref(h)) == L.E_INVALID
     bad = L.Config(n=4, f=1, instances=1, delay_max=17, delay_const=1, key_window=4, variants=1)
     assert lib.brc_create(ctypes.byref(bad), ctypes.byref(h)) == L.E_INVALID

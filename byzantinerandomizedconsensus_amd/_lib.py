@@ -31,7 +31,7 @@ EV_DELIVER, EV_DECIDE, EV_SEND = 1, 2, 3
 
 EXPORTS = ["brc_create", "brc_load_proposals", "brc_load_byzantine", "brc_inject", "brc_run",
            "brc_reset", "brc_read_instances", "brc_read_replicas", "brc_read_events",
-           "brc_read_stats", "brc_last_kernel_ms", "brc_device_count", "brc_last_error",
+           "brc_read_stats", "brc_read_round_histogram", "brc_last_kernel_ms", "brc_device_count", "brc_last_error",
            "brc_destroy", "brc_abi_version"]
 
 
@@ -118,6 +118,7 @@ def load():
         "brc_read_replicas": ([vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ReplicaResult)], ctypes.c_int),
         "brc_read_events": ([vp, ctypes.POINTER(Event), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "brc_read_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
+        "brc_read_round_histogram": ([vp, ctypes.c_void_p, ctypes.c_uint32], ctypes.c_int),
         "brc_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
         "brc_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "brc_last_error": ([vp], ctypes.c_char_p),

@@ -69,6 +69,34 @@ __global__ void reset_slots(uint64_t* meta, uint32_t* mgen, uint64_t keys) {
     if (i < keys) { meta[i] = 0; mgen[i] &= GEN_MASK; }
 }
 
+// Decide-round histogram: per instance, the round by which EVERY honest replica
+// had decided (max of the first-decide rounds); bin 0 = some honest replica never decided; rounds
+// >= bins-1 share the last bin.  One thread per instance; the bins are reduced in LDS first.
+__global__ void round_histogram(const uint64_t* cons1, const uint64_t* byz, uint64_t instances, uint32_t ipw,
+                                uint32_t lpi, uint32_t npad, uint32_t bw, uint32_t n, uint32_t bins,
+                                unsigned long long* hist) {
+    extern __shared__ unsigned long long sh[];
+    for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x) sh[b] = 0;
+    __syncthreads();
+    const uint64_t in = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (in < instances) {
+        const uint64_t item = in / ipw, seg = in % ipw;
+        uint32_t worst = 0;
+        bool all = true;
+        for (uint32_t d = 0; d < n; ++d) {
+            if ((byz[in * bw + d / 64] >> (d % 64)) & 1ull) continue;
+            const uint64_t c1 = cons1[item * lpi + seg * npad + d];
+            if ((c1 & 0xFFFF) == 0) { all = false; break; }
+            worst = max(worst, (uint32_t)((c1 >> 16) & 0xFFFF));
+        }
+        const uint32_t bin = all ? min(worst, bins - 1) : 0u;
+        atomicAdd(&sh[bin], 1ull);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < bins; b += blockDim.x)
+        if (sh[b]) atomicAdd(&hist[b], sh[b]);
+}
+
 __global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) p[i] = v;
@@ -82,6 +110,7 @@ struct Engine {
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
+    uint64_t cons_bytes = 0;                     // consensus-set buffer (hmask) bytes per item
     uint64_t nitems = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -127,15 +156,16 @@ static uint64_t word_mask(uint32_t n, uint32_t w) {
 
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
-static int launch_step(int npad, int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t st, const Params* P) {
+static int launch_step(int npad, int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t st,
+                       const Params* P) {
     switch (npad) {
-    case 4: return launch_step_4(dm, events, blocks, lds, st, P);
-    case 8: return launch_step_8(dm, events, blocks, lds, st, P);
-    case 16: return launch_step_16(dm, events, blocks, lds, st, P);
-    case 32: return launch_step_32(dm, events, blocks, lds, st, P);
-    case 64: return launch_step_64(dm, events, blocks, lds, st, P);
-    case 128: return launch_step_128(dm, events, blocks, lds, st, P);
-    case 256: return launch_step_256(dm, events, blocks, lds, st, P);
+    case 4: return launch_step_4(dm, events, spec, blocks, lds, st, P);
+    case 8: return launch_step_8(dm, events, spec, blocks, lds, st, P);
+    case 16: return launch_step_16(dm, events, spec, blocks, lds, st, P);
+    case 32: return launch_step_32(dm, events, spec, blocks, lds, st, P);
+    case 64: return launch_step_64(dm, events, spec, blocks, lds, st, P);
+    case 128: return launch_step_128(dm, events, spec, blocks, lds, st, P);
+    case 256: return launch_step_256(dm, events, spec, blocks, lds, st, P);
     default: return BRC_E_INVALID;
     }
 }
@@ -172,7 +202,7 @@ static int clear_state(Engine* e, bool full) {
     HIPCHK(e, hipMemsetAsync(e->istats, 0, (size_t)e->cfg.instances * 4 * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->cons0, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->cons1, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * 4 * e->lpi * e->msize, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * e->cons_bytes, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount, 0, 8 * 8, e->stream));
     if (e->event_count) HIPCHK(e, hipMemsetAsync(e->event_count, 0, 8, e->stream));
     return BRC_OK;
@@ -263,9 +293,8 @@ int brc_create(const brc_config* cfg, void** out) {
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
         c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_SPEC ||
-        (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE))
+        (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE) || (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
         return BRC_E_INVALID;
-    if (c.mode != BRC_MODE_REFERENCE) return BRC_E_UNSUPPORTED;
     Engine* e = new Engine();
     e->cfg = c;
     e->npad = pick_npad(c.n);
@@ -279,8 +308,11 @@ int brc_create(const brc_config* cfg, void** out) {
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
-    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max))
-                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, delay_values(c.delay_model, c.delay_max)) * WPB;
+    const bool spec = c.mode == BRC_MODE_SPEC;
+    const uint32_t nL = delay_values(c.delay_model, c.delay_max);
+    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, nL, spec, c.key_window)
+                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window) * WPB;
+    e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window);
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) { delete e; return BRC_E_INVALID; }
     auto fail = [&](int code) { free_all(e); delete e; return code; };
     if (hipSetDevice(c.device) != hipSuccess) { delete e; return BRC_E_HIP; }
@@ -294,7 +326,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},
-        {&e->hmask, (size_t)e->nitems * 4 * e->lpi * e->msize}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
+        {&e->hmask, (size_t)e->nitems * e->cons_bytes}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
     };
@@ -447,6 +479,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.max_steps = max_steps ? max_steps : 0xFFFFFFFFu;
     P.nL = delay_values(c.delay_model, c.delay_max);
     P.event_cap = c.event_capacity;
+    P.mode = c.mode; P.coin_seed = c.coin_seed;
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
@@ -457,7 +490,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
-    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, blocks, e->lds_bytes, e->stream, e->dparams);
+    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, c.mode == BRC_MODE_SPEC, blocks, e->lds_bytes, e->stream,
+                     e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
@@ -603,6 +637,26 @@ int brc_read_stats(void* h, brc_stats* out) {
         HIPCHK(e, hipMemcpy(&n, e->event_count, 8, hipMemcpyDeviceToHost));
         out->events_dropped = n > e->cfg.event_capacity ? n - e->cfg.event_capacity : 0;
     }
+    return BRC_OK;
+}
+
+int brc_read_round_histogram(void* h, uint64_t* hist, uint32_t bins) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || !hist || bins < 2 || bins > 4096) return BRC_E_INVALID;
+    if (e->cfg.protocol != BRC_PROTO_CONSENSUS) { e->err = "round histogram needs the consensus protocol"; return BRC_E_STATE; }
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    unsigned long long* dh = nullptr;
+    HIPCHK(e, hipMalloc(&dh, (size_t)bins * 8));
+    if (hipMemsetAsync(dh, 0, (size_t)bins * 8, e->stream) != hipSuccess) { (void)hipFree(dh); return BRC_E_HIP; }
+    const uint32_t tpb = 256;
+    const uint32_t blocks = (uint32_t)((e->cfg.instances + tpb - 1) / tpb);
+    hipLaunchKernelGGL(round_histogram, dim3(blocks), dim3(tpb), (size_t)bins * 8, e->stream, e->cons1, e->byz,
+                       e->cfg.instances, (uint32_t)e->ipw, e->lpi, (uint32_t)e->npad, e->bw, e->cfg.n, bins, dh);
+    hipError_t r = hipGetLastError();
+    if (r == hipSuccess) r = hipMemcpyAsync(hist, dh, (size_t)bins * 8, hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(dh);
+    if (r != hipSuccess) { e->err = std::string("round histogram: ") + hipGetErrorString(r); return BRC_E_HIP; }
     return BRC_OK;
 }
 

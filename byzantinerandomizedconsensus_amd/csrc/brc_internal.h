@@ -40,6 +40,8 @@ struct Params {
     uint32_t T_echo, T_amp, T_del, T_cnt, bound_p1, bound_p2;
     uint64_t seed, inst_offset, instances, nitems;
     uint32_t max_steps, nL;   // nL: delay_values() of the run
+    uint32_t mode, pad0;      // BRC_MODE_*
+    uint64_t coin_seed;
     uint64_t event_cap;
     uint64_t* cells;
     uint64_t* meta; uint32_t* mgen; uint64_t* kdst;
@@ -57,35 +59,53 @@ __host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) 
     return model == BRC_DELAY_CONST ? 1u : model == BRC_DELAY_SLOWSET ? (dmax > 1 ? 2u : 1u) : dmax;
 }
 
+// u64 words of a wave's consensus LDS area: REFERENCE hm[4][64] T; SPEC seen[Q][64] T + cnt[Q][64] u32
+__host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32_t Q) {
+    return spec ? (Q * 64 * msize + Q * 64 * 4 + 7) / 8 : (4 * 64 * msize + 7) / 8;
+}
+
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
-// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32 |
-// klist[NK] u32
-__host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL) {
+// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
+// mgen[IPW*NK] u32 | klist[NK] u32
+__host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
+                                                       uint32_t Q) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
-    const uint32_t h_words = (4 * 64 * msize + 7) / 8;
+    const uint32_t h_words = cons_words(spec, msize, Q);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 1) / 2);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
-// meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 | hm[4][NW][NPAD] u64 |
+// meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 | consensus area |
 // xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 | klist[NK] u32 | red[12] u32
-__host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL) {
+// consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32 (one key variant per origin)
+__host__ __device__ inline uint32_t cons_words_wide(bool spec, uint32_t npad, uint32_t Q) {
+    const uint32_t nw = npad / 64;
+    return spec ? (Q * npad + 1) / 2 : 4 * nw * npad;
+}
+__host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec, uint32_t Q) {
     const uint32_t nw = (uint32_t)npad / 64;
-    return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + 4 * nw * (uint32_t)npad + 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
+    return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
+                2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
            4 * (NK + NK + 12);
+}
+
+// Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of
+// n bits; SPEC phase windows seen[Q][lanes] (n bits; narrow kernel only) + cnt[Q][lanes] u32.
+inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32_t msize, uint32_t Q) {
+    return spec ? (uint64_t)Q * lanes * ((wide ? 0 : msize) + 4) : 4ull * lanes * msize;
 }
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
-int launch_step_4(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_8(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_16(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_32(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_64(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_4(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_8(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_16(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_32(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_64(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 // wide kernel (brc_step_wide.h): one workgroup of NPAD threads per instance
-int launch_step_128(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_256(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_128(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_256(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 
 }  // namespace brc

@@ -155,11 +155,29 @@ __device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint
     ready_send = r1 || r2;
 }
 
+// Bracha's broadcast as core/brbroadcast.py:60-119 intends it (BRC_MODE_SPEC; oracle
+// brb_on_message_spec): ECHO on the first SEND of a key, ONE READY per key -- at the echo quorum or
+// at f+1 READYs --, DELIVER at 2f+1 READYs, everything after DELIVER ignored.  All ECHOs of a step
+// precede its READYs, so the sequential checks reduce to the step's final set sizes.
+__device__ __forceinline__ void brb_cell_update_spec(uint32_t& fl, uint32_t& ec, uint32_t& rc, bool s_arr,
+                                                     uint32_t ea, uint32_t ra, uint32_t T_echo, uint32_t T_amp,
+                                                     uint32_t T_del, bool& echo_send, bool& ready_send, bool& deliver) {
+    const bool open = !(fl & F_DEL);
+    echo_send = open && s_arr && !(fl & F_ES);
+    fl |= echo_send ? F_ES : 0u;
+    ec += open ? ea : 0u;
+    rc += open ? ra : 0u;
+    ready_send = open && !(fl & F_RS) && (ec >= T_echo || rc >= T_amp);
+    fl |= ready_send ? F_RS : 0u;
+    deliver = open && rc >= T_del;
+    fl |= deliver ? F_DEL : 0u;
+}
+
 #ifndef BRC_MIN_WAVES
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
 
-template <int NPAD, int DM, bool EV>
+template <int NPAD, int DM, bool EV, bool SPEC>
 __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params* pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
@@ -175,14 +193,17 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
-    //     dbits[nkw][64] u64 | hm[4][64] T | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK] u32
+    //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK] u32
+    // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
     const uint32_t nL = P.nL;
-    constexpr uint32_t h_words = (4 * 64 * (uint32_t)sizeof(T) + 7) / 8;
+    const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q);
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL) / 8);
+    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q) / 8);
     uint64_t* s_act = s_meta + IPW * NK;
     uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
     T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
+    T* s_seen = s_hm;                            // SPEC: s_seen[q*64 + lane]: hosts delivered for phase slot q
+    uint32_t* s_cnt = (uint32_t*)(s_seen + Q * 64); // SPEC: s_cnt[q*64 + lane]: #"0" | #"1" << 16
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
     uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
     uint32_t* s_klist = s_gen + ((IPW * NK + 1) & ~1u); // this step's active key slots
@@ -286,7 +307,16 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     const size_t li = item * 64 + lane;
     const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
     if (cons_lane) { c0 = gp(P.cons0)[li]; c1 = gp(P.cons1)[li]; }
-    for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? gp((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
+    if constexpr (SPEC) {
+        const T* gseen = (const T*)P.hmask;
+        const uint32_t* gcnt = (const uint32_t*)((const char*)P.hmask + P.nitems * Q * 64 * sizeof(T));
+        for (uint32_t q = 0; q < Q; ++q) {
+            s_seen[q * 64 + lane] = cons_lane ? gp(gseen)[(item * Q + q) * 64 + lane] : (T)0;
+            s_cnt[q * 64 + lane] = cons_lane ? gp(gcnt)[(item * Q + q) * 64 + lane] : 0u;
+        }
+    } else {
+        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? gp((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
+    }
     uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
     uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
@@ -363,6 +393,56 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         }
     };
 
+    // ---- SPEC consensus (oracle spec_advance / spec_deliver): the protocol
+    // core/byzantinerandomizedconsensus.py:53-106 intends -- a phase ends once n-f DISTINCT origins
+    // delivered a key of THAT phase (deliveries of later phases are buffered in slot s % Q, earlier
+    // ones dropped); phase 1 proposes a value carried by more than (n+f)/2 of them (:73), phase 2
+    // decides above 2f (:88), adopts above f and otherwise takes the common coin (:90-92, reachable
+    // here), then the next round starts.
+    auto spec_advance = [&]() {
+        while (round > 0) {
+            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s % Q;
+            if (popc(s_seen[q * 64 + lane]) < n - P.f) return;
+            const uint32_t cc = s_cnt[q * 64 + lane], n0 = cc & 0xFFFF, n1 = cc >> 16;
+            s_seen[q * 64 + lane] = 0;
+            s_cnt[q * 64 + lane] = 0;
+            if (phase == 1) {
+                const uint32_t prop = (2 * n0 > n + P.f) ? 1u : (2 * n1 > n + P.f) ? 2u : 0u;
+                phase = 2;
+                send_key(s + 1, prop);
+            } else {
+                const uint32_t vmax = n1 > n0 ? 2u : 1u, cmax = max(n0, n1);
+                uint32_t est;
+                if (cmax > 2 * P.f) {
+                    ++dcount;
+                    if (dcount == 1) { frnd = round; ft = t; fval = vmax; }
+                    lval = vmax;
+                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax);
+                    est = vmax;
+                } else if (cmax > P.f) {
+                    est = vmax;
+                } else {
+                    est = coin_id(P.coin_seed, g, round);
+                }
+                ++round; phase = 1;
+                send_key(s + 1, est);
+            }
+        }
+    };
+    auto spec_deliver = [&](uint32_t k) {
+        const uint64_t m = s_meta[mbase + k];
+        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = (k / Q) / NV;
+        const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
+        if (s < cur) return;
+        if (s >= cur + Q) { ovf = true; return; }
+        const uint32_t q = s % Q;
+        if ((s_seen[q * 64 + lane] >> host) & 1) return;
+        s_seen[q * 64 + lane] |= (T)((T)1 << host);
+        if (v == 1) s_cnt[q * 64 + lane] += 1u;
+        else if (v == 2) s_cnt[q * 64 + lane] += 1u << 16;
+        spec_advance();
+    };
+
     // ---- actions stamped t (performed after step t's messages)
     auto do_actions = [&]() -> bool {
         bool mine_any = false;
@@ -373,6 +453,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                                                                          : (uint32_t)gp(P.prop)[inst * n + d];
                 round = 1; phase = 1;                                 // :43-47
                 send_key(0, v & 3);
+                if constexpr (SPEC) spec_advance();                   // phase 0 may be buffered
             }
         }
         while (inj_pos < inj_cnt) {
@@ -382,7 +463,10 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             const bool mine = running && seg == (int)r.seg;
             mine_any |= mine;
             if (r.kind == BRC_INJ_PROPOSE) {
-                if (mine && honest && d == r.node) { round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3); }
+                if (mine && honest && d == r.node) {
+                    round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
+                    if constexpr (SPEC) spec_advance();
+                }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the
                 // slot first unless that key was declared and not yet sent
@@ -547,7 +631,8 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             st_loads += (kl && real_run) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
             bool es, rs, dl;
-            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {   // whole-wave store (lanes without arrivals write their word back unchanged)
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
@@ -632,7 +717,8 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                             }
                         }
                         grp &= ~(1ull << best);
-                        cons_deliver(w * 64 + best);
+                        if constexpr (SPEC) spec_deliver(w * 64 + best);
+                        else cons_deliver(w * 64 + best);
                     }
                 }
             }
@@ -685,7 +771,16 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                       ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
         gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                       ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
-        for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
+        if constexpr (SPEC) {
+            T* gseen = (T*)P.hmask;
+            uint32_t* gcnt = (uint32_t*)((char*)P.hmask + P.nitems * Q * 64 * sizeof(T));
+            for (uint32_t q = 0; q < Q; ++q) {
+                gp(gseen)[(item * Q + q) * 64 + lane] = s_seen[q * 64 + lane];
+                gp(gcnt)[(item * Q + q) * 64 + lane] = s_cnt[q * 64 + lane];
+            }
+        } else {
+            for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
+        }
     }
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
@@ -721,10 +816,10 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     }
 }
 
-// Launch one (DM, EV) instantiation of the step kernel for a fixed NPAD.
-template <int NPAD, int DMX, bool EV>
+// Launch one (DM, EV, SPEC) instantiation of the step kernel for a fixed NPAD.
+template <int NPAD, int DMX, bool EV, bool SPEC>
 int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step<NPAD, DMX, EV>;
+    auto kern = brc_step<NPAD, DMX, EV, SPEC>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -733,10 +828,14 @@ int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 }
 
 template <int NPAD>
-int launch_step(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-#define BRC_CASE(DMX)                                                                         \
-    if (dm == DMX) return events ? launch_one<NPAD, DMX, true>(blocks, lds, s, P)             \
-                                 : launch_one<NPAD, DMX, false>(blocks, lds, s, P);
+int launch_step(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+#define BRC_CASE(DMX)                                                                                  \
+    if (dm == DMX) {                                                                                   \
+        if (spec) return events ? launch_one<NPAD, DMX, true, true>(blocks, lds, s, P)                 \
+                                : launch_one<NPAD, DMX, false, true>(blocks, lds, s, P);               \
+        return events ? launch_one<NPAD, DMX, true, false>(blocks, lds, s, P)                          \
+                      : launch_one<NPAD, DMX, false, false>(blocks, lds, s, P);                        \
+    }
 #ifdef BRC_ONLY_DM8
     BRC_CASE(8)
 #else

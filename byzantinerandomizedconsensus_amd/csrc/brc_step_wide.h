@@ -41,7 +41,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return x;
 }
 
-template <int NPAD, int DM, bool EV>
+template <int NPAD, int DM, bool EV, bool SPEC>
 __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const Params& P = *pp;
     constexpr int NW = NPAD / 64;
@@ -54,13 +54,18 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw, nL = P.nL;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del, model = P.delay_model;
     // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 |
-    //   hm[4][NW][NPAD] u64 | xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
+    //   consensus area | xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
     //   klist[NK] u32 | red[3][4] u32
+    // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32
     uint64_t* s_meta = smem;
     uint64_t* s_act = s_meta + NK;
     uint64_t* s_dbits = s_act + TS * nkw;
     uint64_t* s_hm = s_dbits + (size_t)nkw * NPAD;
-    uint64_t* s_xb = s_hm + 4 * NW * NPAD;
+    // SPEC, per phase slot q = s % Q: #origins | #"0" << 10 | #"1" << 20.  The wide engine takes
+    // one key variant per origin (brc_create), so a replica delivers each (origin, phase) key at
+    // most once and the origin count needs no host set.
+    uint32_t* s_cnt = (uint32_t*)s_hm;
+    uint64_t* s_xb = s_hm + cons_words_wide(SPEC, NPAD, Q);
     uint64_t* s_outm = s_xb + 2 * CHUNK_W * nL * 2 * NW;
     uint32_t* s_gen = (uint32_t*)(s_outm + 16 * NW);
     uint32_t* s_klist = s_gen + NK;
@@ -200,9 +205,15 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const bool cons_lane = honest && P.protocol == BRC_PROTO_CONSENSUS;
     if (cons_lane) { c0 = gp(P.cons0)[li]; c1 = gp(P.cons1)[li]; }
     auto hm = [&](uint32_t v, uint32_t w) -> uint64_t& { return s_hm[(v * NW + w) * NPAD + d]; };
-    for (uint32_t v = 0; v < 4; ++v)
-        for (uint32_t w = 0; w < NW; ++w)
-            hm(v, w) = cons_lane ? gp((const uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] : 0ull;
+    auto cnt = [&](uint32_t q) -> uint32_t& { return s_cnt[q * NPAD + d]; };
+    const gptr_t<uint32_t> gcnt = gp((uint32_t*)P.hmask);
+    if constexpr (SPEC) {
+        for (uint32_t q = 0; q < Q; ++q) cnt(q) = cons_lane ? gcnt[(inst * Q + q) * NPAD + d] : 0u;
+    } else {
+        for (uint32_t v = 0; v < 4; ++v)
+            for (uint32_t w = 0; w < NW; ++w)
+                hm(v, w) = cons_lane ? gp((const uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] : 0ull;
+    }
     uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
     uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
@@ -303,6 +314,47 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         }
     };
 
+    // ---- SPEC consensus (as brc_step.h spec_advance / spec_deliver)
+    auto spec_advance = [&]() {
+        while (round > 0) {
+            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s % Q;
+            const uint32_t cc = cnt(q), n0 = (cc >> 10) & 0x3FF, n1 = cc >> 20;
+            if ((cc & 0x3FF) < n - P.f) return;
+            cnt(q) = 0;
+            if (phase == 1) {
+                const uint32_t prop = (2 * n0 > n + P.f) ? 1u : (2 * n1 > n + P.f) ? 2u : 0u;
+                phase = 2;
+                send_key(s + 1, prop);
+            } else {
+                const uint32_t vmax = n1 > n0 ? 2u : 1u, cmax = max(n0, n1);
+                uint32_t est;
+                if (cmax > 2 * P.f) {
+                    ++dcount;
+                    if (dcount == 1) { frnd = round; ft = t; fval = vmax; }
+                    lval = vmax;
+                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax);
+                    est = vmax;
+                } else if (cmax > P.f) {
+                    est = vmax;
+                } else {
+                    est = coin_id(P.coin_seed, g, round);
+                }
+                ++round; phase = 1;
+                send_key(s + 1, est);
+            }
+        }
+    };
+    auto spec_deliver = [&](uint32_t k) {
+        const uint64_t m = s_meta[k];
+        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = (k / Q) / NV;
+        const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
+        if (s < cur) return;
+        if (s >= cur + Q) { ovf = true; return; }
+        (void)host;
+        cnt(s % Q) += 1u + (v == 1 ? 1u << 10 : 0u) + (v == 2 ? 1u << 20 : 0u);
+        spec_advance();
+    };
+
     // ---- actions stamped t (performed after step t's messages); every branch is workgroup-uniform
     auto do_actions = [&]() -> bool {
         bool mine_any = false;
@@ -313,6 +365,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                                                                          : (uint32_t)gp(P.prop)[inst * n + d];
                 round = 1; phase = 1;                                 // :43-47
                 send_key(0, v & 3);
+                if constexpr (SPEC) spec_advance();                   // phase 0 may be buffered
             }
         }
         while (inj_pos < inj_cnt) {
@@ -322,7 +375,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             const bool mine = running;
             mine_any |= mine;
             if (r.kind == BRC_INJ_PROPOSE) {
-                if (mine && honest && d == r.node) { round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3); }
+                if (mine && honest && d == r.node) {
+                    round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
+                    if constexpr (SPEC) spec_advance();
+                }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // every peer is a destination (brc_inject rejects restricted SENDs for n > 64)
                 const bool is_send = r.kind == BRC_INJ_SEND;
@@ -491,7 +547,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             st_loads += (kl && real) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 255, rc = (uint32_t)(word >> 13) & 255;
             bool es, rs, dl;
-            brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)min(ec, 255u) << 5) | ((uint64_t)min(rc, 255u) << 13) |
@@ -575,7 +632,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                             }
                         }
                         grp &= ~(1ull << best);
-                        cons_deliver(w * 64 + best);
+                        if constexpr (SPEC) spec_deliver(w * 64 + best);
+                        else cons_deliver(w * 64 + best);
                     }
                 }
             }
@@ -614,8 +672,12 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                           ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
         gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                           ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
-        for (uint32_t v = 0; v < 4; ++v)
-            for (uint32_t w = 0; w < NW; ++w) gp((uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] = hm(v, w);
+        if constexpr (SPEC) {
+            for (uint32_t q = 0; q < Q; ++q) gcnt[(inst * Q + q) * NPAD + d] = cnt(q);
+        } else {
+            for (uint32_t v = 0; v < 4; ++v)
+                for (uint32_t w = 0; w < NW; ++w) gp((uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] = hm(v, w);
+        }
     }
     // statistics: wave sums, then one atomic per wave and counter
     uint64_t w6[5] = {st_cells, st_arr, st_msgs, st_del, st_loads};
@@ -642,9 +704,9 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     }
 }
 
-template <int NPAD, int DMX, bool EV>
+template <int NPAD, int DMX, bool EV, bool SPEC>
 int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step_wide<NPAD, DMX, EV>;
+    auto kern = brc_step_wide<NPAD, DMX, EV, SPEC>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -653,10 +715,14 @@ int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* 
 }
 
 template <int NPAD>
-int launch_step_wide(int dm, bool events, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-#define BRC_CASE(DMX)                                                                         \
-    if (dm == DMX) return events ? launch_wide_one<NPAD, DMX, true>(blocks, lds, s, P)        \
-                                 : launch_wide_one<NPAD, DMX, false>(blocks, lds, s, P);
+int launch_step_wide(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+#define BRC_CASE(DMX)                                                                                  \
+    if (dm == DMX) {                                                                                   \
+        if (spec) return events ? launch_wide_one<NPAD, DMX, true, true>(blocks, lds, s, P)            \
+                                : launch_wide_one<NPAD, DMX, false, true>(blocks, lds, s, P);          \
+        return events ? launch_wide_one<NPAD, DMX, true, false>(blocks, lds, s, P)                     \
+                      : launch_wide_one<NPAD, DMX, false, false>(blocks, lds, s, P);                   \
+    }
     BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
 #undef BRC_CASE
     return BRC_E_INVALID;

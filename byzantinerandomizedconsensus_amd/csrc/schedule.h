@@ -54,4 +54,9 @@ __host__ __device__ inline uint32_t proposal_id(uint64_t seed, uint64_t g, uint3
     return 1u + (draw(seed, g, i, PURPOSE_PROPOSAL, 0).x & 1u);
 }
 
+// BRC_MODE_SPEC common coin of (instance, round): value id 1 ("0") or 2 ("1")
+__host__ __device__ inline uint32_t coin_id(uint64_t coin_seed, uint64_t g, uint32_t round) {
+    return 1u + (draw(coin_seed, g, round, PURPOSE_COIN, 0).x & 1u);
+}
+
 }  // namespace brc

@@ -144,6 +144,13 @@ class Engine:
                                 % (cnt.value, self.cfg.event_capacity))
         return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b) for e in arr[:cap]]
 
+    def round_histogram(self, bins=66):
+        """hist[r] = instances whose honest replicas had all decided by round r; hist[0] =
+        instances with an undecided honest replica; the last bin holds rounds >= bins - 1."""
+        arr = np.zeros(bins, dtype=np.uint64)
+        self._chk(self._lib.brc_read_round_histogram(self._h, arr.ctypes.data_as(ctypes.c_void_p), bins))
+        return [int(x) for x in arr]
+
     def stats(self):
         s = L.Stats()
         self._chk(self._lib.brc_read_stats(self._h, ctypes.byref(s)))

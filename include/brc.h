@@ -141,6 +141,11 @@ int brc_read_instances(void* engine, uint64_t first, uint64_t count, brc_instanc
 int brc_read_replicas(void* engine, uint64_t first, uint64_t count, brc_replica_result* out /* [count][n] */);
 int brc_read_events(void* engine, brc_event* out, size_t cap, size_t* count);
 int brc_read_stats(void* engine, brc_stats* out);
+/* Decide-round histogram over instances (consensus): hist[r] = instances whose honest replicas
+ * had ALL decided by round r (the max of their first-decide rounds), hist[0] = instances with an
+ * undecided honest replica, rounds >= bins-1 in hist[bins-1].  bins in [2, 4096].  Per engine
+ * (= per GPU shard); SURVEY §8(d) cfg5 all-reduces it over ranks (shard.reduce_stats). */
+int brc_read_round_histogram(void* engine, uint64_t* hist, uint32_t bins);
 int brc_last_kernel_ms(void* engine, float* ms);
 int brc_device_count(int* count);
 const char* brc_last_error(void* engine);

@@ -23,7 +23,7 @@ def sort_result(res):
 def _cfg_key(sp):
     return (sp["n"], sp["f"], sp["mode"], sp.get("nv", 1), sp["seed"], sp["delay_model"], sp["dmax"],
             sp.get("dconst", 1), sp.get("round_cap", 0), sp.get("step_cap", 10000),
-            tuple(sorted(sp.get("byzantine", []))))
+            tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"))
 
 
 def _injections(sp, local):
@@ -59,13 +59,18 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
     """specs share _cfg_key and have consecutive g.  The key window defaults to the widest
     the engine allows (Q * NV <= 8)."""
     sp0 = specs[0]
-    if key_window is None:
+    spec_mode = sp0["mode"] in ("spec", "spec_brb")
+    if spec_mode:
+        key_window = sp0["window"]          # the SPEC buffering window IS the engine's key window
+    elif key_window is None:
         key_window = 8 // sp0.get("nv", 1)
-    eng = Engine(n=sp0["n"], f=sp0["f"], instances=len(specs), protocol=sp0["mode"], seed=sp0["seed"],
+    protocol = {"spec": "consensus", "spec_brb": "brb"}.get(sp0["mode"], sp0["mode"])
+    eng = Engine(n=sp0["n"], f=sp0["f"], instances=len(specs), protocol=protocol, seed=sp0["seed"],
                  delay_model=sp0["delay_model"], delay_max=sp0["dmax"], delay_const=sp0.get("dconst", 1),
                  round_cap=sp0.get("round_cap", 0), step_cap=sp0.get("step_cap", 10000), key_window=key_window,
                  variants=sp0.get("nv", 1), byzantine=sp0.get("byzantine", ()), event_capacity=event_capacity,
-                 instance_offset=sp0["g"], device=device)
+                 instance_offset=sp0["g"], device=device, mode=L.MODE_SPEC if spec_mode else L.MODE_REFERENCE,
+                 coin_seed=sp0.get("coin_seed", 0))
     try:
         inj = []
         for i, sp in enumerate(specs):

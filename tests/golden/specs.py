@@ -51,6 +51,21 @@ def cons_spec(n, f, seed, model, dmax, g, round_cap=2, proposals=None, byzantine
                 step_cap=step_cap, actions=acts)
 
 
+def spec_cons_spec(n, f, seed, model, dmax, g, round_cap=1, window=4, coin_seed=0xC01D, **kw):
+    """BRC_MODE_SPEC consensus (tests/spec_model.py): the intended protocol, common coin keyed
+    (coin_seed, g, round); ``window`` = phase indices a replica buffers (the engine's key window)."""
+    sp = cons_spec(n, f, seed, model, dmax, g, round_cap=round_cap, **kw)
+    sp.update(mode="spec", window=window, coin_seed=coin_seed)
+    return sp
+
+
+def spec_brb_spec(n, f, seed, model, dmax, g, sends, window=4, **kw):
+    """BRC_MODE_SPEC broadcast only (Bracha-correct BRB)."""
+    sp = brb_spec(n, f, seed, model, dmax, g, sends, **kw)
+    sp.update(mode="spec_brb", window=window, coin_seed=0)
+    return sp
+
+
 def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
     """SURVEY §8(d) cfg3 pattern: each Byzantine replica b SENDs value "0" to even
     destinations and "1" to odd ones, then ECHOes and READYs both keys to everyone."""

@@ -24,7 +24,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-N_REPLICAS, F_FAULTS, DELAY_MAX, SEED = 64, 21, 8, 0x5EED0004
+N_REPLICAS, F_FAULTS, DELAY_MAX, SEED, COIN_SEED = 64, 21, 8, 0x5EED0004, 0xC017C017
 SURVEY_BYTES_PER_CELL_STEP = 6 * ((N_REPLICAS + 7) // 8) + 2   # 50 B at n=64
 HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
 
@@ -35,13 +35,17 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 17, help="instances per GPU")
-    ap.add_argument("--key-window", type=int, default=4)
+    ap.add_argument("--key-window", type=int, default=0, help="0: 4 (reference mode), 8 (spec mode)")
+    ap.add_argument("--mode", choices=("reference", "spec"), default="reference",
+                    help="reference: the protocol as the reference runs it (headline); spec: the intended "
+                         "protocol with its common coin (SURVEY §8 F3)")
+    ap.add_argument("--round-cap", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
+def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
     """The C oracle (a scalar port of the reference's path, 1 core) on the same workload:
     the first instances of the batch, until `seconds` of CPU work have been spent."""
     from oracle import oracle
@@ -49,7 +53,11 @@ def cpu_baseline(seconds):
     t0 = time.perf_counter()
     done = arrivals = count = 0
     while time.perf_counter() - t0 < seconds:
-        sp = S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, count, round_cap=1)
+        if mode == "spec":
+            sp = S.spec_cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, count, round_cap=round_cap,
+                                  window=window, coin_seed=COIN_SEED)
+        else:
+            sp = S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, count, round_cap=round_cap)
         r = oracle.run(sp)
         done += r["status"] == "done"
         arrivals += r["arrivals"]
@@ -61,7 +69,7 @@ def cpu_baseline(seconds):
                       % (count, count - 1, dt, arrivals / dt)}
 
 
-def load_traffic(instances, kernel_ms):
+def load_traffic(instances, kernel_ms, mode="reference"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
     written by profiles/summarize.py), used only if it was taken on this workload and size and
     its kernel time agrees with the live one within 15 % (i.e. the same kernel build)."""
@@ -71,7 +79,8 @@ def load_traffic(instances, kernel_ms):
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    if d.get("instances") != instances or d.get("workload") != "cfg4" or not d.get("avg_ns"):
+    if d.get("instances") != instances or d.get("workload") != "cfg4" or not d.get("avg_ns") or \
+            d.get("mode", "reference") != mode:
         return None
     if abs(d["avg_ns"] / 1e6 - kernel_ms) > 0.15 * kernel_ms:
         return None
@@ -96,11 +105,15 @@ def main():
     from byzantinerandomizedconsensus_amd.engine import Engine
 
     per = args.instances
+    spec = args.mode == "spec"
+    if not args.key_window:
+        args.key_window = 8 if spec else 4
     first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
     eng = Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
-                 delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=1, step_cap=4000,
+                 delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=args.round_cap, step_cap=4000,
                  key_window=args.key_window, variants=1, proposals=L.PROPOSALS_PHILOX,
-                 instance_offset=first, device=local)
+                 instance_offset=first, device=local, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
+                 coin_seed=COIN_SEED)
 
     def barrier():
         if dist is not None:
@@ -125,7 +138,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(kms) / len(kms)
     # the only collective: statistics (RCCL over xGMI), max of the wall clocks
-    st, _ = shard.reduce_stats(eng.stats(), dist, device="cuda")
+    st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(66))
     elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
     kernel_ms = shard.max_over_ranks(kernel_ms, dist, device="cuda")
     decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
@@ -136,7 +149,7 @@ def main():
     out = None
     if rank == 0:
         achieved = SURVEY_BYTES_PER_CELL_STEP * (cell_steps / world) / (kernel_ms / 1e3) / 1e9
-        traffic = load_traffic(per, kernel_ms)
+        traffic = load_traffic(per, kernel_ms, args.mode)
         out = {
             "metric": "decided consensus instances/sec (node) at n=64,f=21",
             "value": value,
@@ -150,10 +163,14 @@ def main():
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
-            "config": {"workload": "cfg4: n=64 f=21 reference-protocol consensus to first decision, "
-                                   "slow-set delays D=8, %d instances/GPU" % per,
-                       "n": N_REPLICAS, "f": F_FAULTS, "instances_per_gpu": per, "round_cap": 1,
-                       "key_window": args.key_window, "parallelism": "instance-sharded x%d" % world},
+            "config": {"workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
+                                   % ("SPEC-protocol (common coin)" if spec else "reference-protocol",
+                                      "first decision" if args.round_cap == 1 else "%d decisions" % args.round_cap,
+                                      per),
+                       "n": N_REPLICAS, "f": F_FAULTS, "instances_per_gpu": per, "round_cap": args.round_cap,
+                       "mode": args.mode, "key_window": args.key_window,
+                       "parallelism": "instance-sharded x%d" % world},
+            "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
             "replica_message_steps_per_s": arrivals * args.steps / world * world / elapsed,
             "decided_fraction": decided / float(per * world),
             "kernel_ms": kernel_ms,
@@ -164,7 +181,7 @@ def main():
         }
     eng.close()
     if rank == 0 and not args.no_cpu and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.mode, args.key_window, args.round_cap)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

@@ -97,9 +97,11 @@ __global__ void round_histogram(const uint64_t* cons1, const uint64_t* byz, uint
         if (sh[b]) atomicAdd(&hist[b], sh[b]);
 }
 
+// grid-stride fill: a dispatch holds < 2^32 work-items per dimension, and the cell array can
+// exceed that (2^17 instances x 512 key slots x 64 lanes = 2^32 words at n = 64, Q = 8)
 __global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) p[i] = v;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) p[i] = v;
 }
 
 // ------------------------------------------------------------------------------------ host
@@ -132,6 +134,8 @@ struct Engine {
     uint64_t gen_budget = 0;                     // generation advance bound since the last full clear
     std::vector<std::pair<uint64_t, uint32_t>> send_keys;   // (instance, kp<<16|s) of injected SENDs
 };
+
+thread_local std::string g_create_err;    // brc_last_error(NULL): the last brc_create failure
 
 #define HIPCHK(e, x)                                                                   \
     do {                                                                               \
@@ -184,8 +188,8 @@ static int clear_state(Engine* e, bool full) {
     const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
     const size_t keys = (size_t)e->cfg.instances * e->NK;
     if (full) {
-        hipLaunchKernelGGL(fill_u64, dim3((uint32_t)((cells + 255) / 256)), dim3(256), 0, e->stream, e->cells,
-                           TIMES_NEVER, (uint64_t)cells);
+        const uint64_t fb = std::min<uint64_t>((cells + 255) / 256, 1u << 20);
+        hipLaunchKernelGGL(fill_u64, dim3((uint32_t)fb), dim3(256), 0, e->stream, e->cells, TIMES_NEVER, (uint64_t)cells);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipMemsetAsync(e->meta, 0, keys * 8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->mgen, 0, keys * 4, e->stream));
@@ -276,12 +280,13 @@ int brc_device_count(int* count) {
 }
 
 const char* brc_last_error(void* h) {
-    if (!h) return "null engine";
+    if (!h) return g_create_err.c_str();   // why the last brc_create on this thread failed
     return static_cast<Engine*>(h)->err.c_str();
 }
 
 int brc_create(const brc_config* cfg, void** out) {
-    if (!cfg || !out) return BRC_E_INVALID;
+    g_create_err.clear();
+    if (!cfg || !out) { g_create_err = "null argument"; return BRC_E_INVALID; }
     *out = nullptr;
     const brc_config& c = *cfg;
     if (c.n < 1 || c.n > 256 || c.instances == 0 || c.delay_max < 1 || c.delay_max > 16 ||
@@ -294,7 +299,10 @@ int brc_create(const brc_config* cfg, void** out) {
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
         c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_SPEC ||
         (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE) || (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
+    {
+        g_create_err = "invalid configuration (see include/brc.h field ranges)";
         return BRC_E_INVALID;
+    }
     Engine* e = new Engine();
     e->cfg = c;
     e->npad = pick_npad(c.n);
@@ -313,9 +321,17 @@ int brc_create(const brc_config* cfg, void** out) {
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, nL, spec, c.key_window)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window);
-    if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) { delete e; return BRC_E_INVALID; }
-    auto fail = [&](int code) { free_all(e); delete e; return code; };
-    if (hipSetDevice(c.device) != hipSuccess) { delete e; return BRC_E_HIP; }
+    if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
+        g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
+        delete e;
+        return BRC_E_INVALID;
+    }
+    auto fail = [&](int code) {
+        g_create_err = e->err.empty() ? std::string("brc_create: HIP call failed: ") + hipGetErrorString(hipGetLastError())
+                                      : e->err;
+        free_all(e); delete e; return code;
+    };
+    if (hipSetDevice(c.device) != hipSuccess) { g_create_err = "hipSetDevice failed"; delete e; return BRC_E_HIP; }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail(BRC_E_HIP);
     if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) return fail(BRC_E_HIP);
     const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
@@ -331,7 +347,10 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->dparams, sizeof(Params)},
     };
     for (auto& a : allocs)
-        if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) return fail(BRC_E_NOMEM);
+        if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) {
+            e->err = "device allocation of " + std::to_string(a.bytes) + " B failed";
+            return fail(BRC_E_NOMEM);
+        }
     if (c.event_capacity) {
         if (hipMalloc(&e->events, (size_t)c.event_capacity * sizeof(brc_event)) != hipSuccess) return fail(BRC_E_NOMEM);
         if (hipMalloc(&e->event_count, 8) != hipSuccess) return fail(BRC_E_NOMEM);

@@ -44,7 +44,8 @@ class Engine:
             self.cfg.byzantine_mask_hi[w] = (mask >> (64 * (w + 1))) & M64
         rc = self._lib.brc_create(ctypes.byref(self.cfg), ctypes.byref(self._h))
         if rc != L.OK:
-            raise L.EngineError(rc, "brc_create rejected the configuration")
+            why = self._lib.brc_last_error(None) or b""
+            raise L.EngineError(rc, "brc_create: %s" % why.decode(errors="replace"))
         self.n, self.f, self.instances = n, f, instances
 
     # ------------------------------------------------------------------ lifecycle

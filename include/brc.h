@@ -148,7 +148,7 @@ int brc_read_stats(void* engine, brc_stats* out);
 int brc_read_round_histogram(void* engine, uint64_t* hist, uint32_t bins);
 int brc_last_kernel_ms(void* engine, float* ms);
 int brc_device_count(int* count);
-const char* brc_last_error(void* engine);
+const char* brc_last_error(void* engine);   /* engine NULL: why the last brc_create on this thread failed */
 void brc_destroy(void* engine);
 int brc_abi_version(void);
 

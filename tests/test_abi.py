@@ -80,3 +80,11 @@ def test_engine_refuses_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(L.EngineUnavailable):
         L.load()
+
+
+def test_create_failure_reason_is_reported():
+    lib = L.load()
+    h = ctypes.c_void_p()
+    bad = L.Config(n=4, f=1, instances=1, delay_max=1, delay_const=1, key_window=3, variants=1)
+    assert lib.brc_create(ctypes.byref(bad), ctypes.byref(h)) == L.E_INVALID
+    assert b"invalid configuration" in lib.brc_last_error(None)

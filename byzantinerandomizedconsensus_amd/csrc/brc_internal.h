@@ -9,7 +9,11 @@
 namespace brc {
 
 constexpr int TS = 32;            // activity ring (steps); > max delay
-constexpr int WPB = 4;            // independent waves per workgroup
+#ifndef BRC_WPB
+#define BRC_WPB 1
+#endif
+constexpr int WPB = BRC_WPB;      // independent waves per workgroup (narrow kernel); 1 measured best:
+                                  // LDS-bound SPEC runs pack more waves per CU (exp/ab.sh, r1)
 constexpr uint32_t NEVER = 0xFFFFu;
 constexpr uint64_t TIMES_NEVER = 0xFFFFFFFF00000000ull;
 constexpr uint32_t F_EEX = 1, F_REX = 2, F_DEL = 4, F_ES = 8, F_RS = 16;

@@ -1,0 +1,158 @@
+"""Full-size GPU runs of BASELINE.json's configurations, checked through properties that do not
+depend on the size: instances drawn from the full batch equal the C oracle run alone on their
+global id (bit-exact status / last step / message counts / decide rounds), results do not depend
+on how the instances are sharded across engines (multi-GPU invariance), and a
+checksum over every instance is identical across shardings.
+
+cfg2: 10,000 instances n=4 f=1, honest, uniform delays [1,4] (one GPU).
+cfg3: one rank's shard of the 1M-instance n=16 f=5 run: 125,000 instances at global offset
+      3 x 125,000, Byzantine {11..15} equivocating.
+cfg4: the bench batch, 131,072 instances n=64 f=21, slow-set delays D=8 (reference and SPEC).
+cfg5: n=256 f=85, 512 instances per delay model (SPEC).
+"""
+import hashlib
+import random
+
+import pytest
+
+from oracle import oracle
+from tests.golden import specs as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(**kw):
+    from byzantinerandomizedconsensus_amd.engine import Engine
+    return Engine(**kw)
+
+
+def _L():
+    from byzantinerandomizedconsensus_amd import _lib as L
+    return L
+
+
+KEYS = ("status", "t_stop", "msgs_sent", "arrivals")
+
+
+def _run(kw, first, count, ids=()):
+    """Run [first, first + count); return every instance's result and the replicas of `ids`."""
+    with _engine(instance_offset=first, instances=count, **kw) as eng:
+        eng.run()
+        res = eng.instances_result()
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    return res, reps
+
+
+def _digest(res):
+    h = hashlib.sha256()
+    for r in res:
+        h.update(repr(tuple(r[k] for k in KEYS)).encode())
+    return h.hexdigest()
+
+
+def _check_sample(res, reps, kw, base, ids, make_spec):
+    for i in ids:
+        sp = make_spec(base + i)
+        exp = oracle.run(sp)
+        for k in KEYS:
+            assert res[i][k] == exp[k], "instance %d %s: engine %r oracle %r" % (base + i, k, res[i][k], exp[k])
+        if i in reps:
+            first = {}
+            for t, node, rnd, val in sorted(exp["events"]["decide"]):
+                first.setdefault(node, (rnd, t))
+            for d, rep in enumerate(reps[i]):
+                if d in sp.get("byzantine", []):
+                    continue
+                if d in first:
+                    assert (rep["first_decide_round"], rep["first_decide_t"]) == first[d], (base + i, d)
+                else:
+                    assert rep["decide_count"] == 0, (base + i, d)
+
+
+def _sharding_invariant(kw, first, count, full):
+    half = count // 2
+    a, _ = _run(kw, first, half)
+    b, _ = _run(kw, first + half, count - half)
+    assert _digest(a + b) == _digest(full)
+
+
+def test_cfg2_full_size():
+    L = _L()
+    N = 10000
+    kw = dict(n=4, f=1, protocol="consensus", seed=0x5EED0002, delay_model=L.DELAY_UNIFORM, delay_max=4,
+              round_cap=2, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX)
+    ids = random.Random(2).sample(range(N), 64)
+    res, reps = _run(kw, 0, N, ids)
+    assert all(r["status"] in ("done", "quiescent") for r in res)
+    _check_sample(res, reps, kw, 0, ids, lambda g: S.cons_spec(4, 1, 0x5EED0002, 1, 4, g, round_cap=2))
+    _sharding_invariant(kw, 0, N, res)
+
+
+def test_cfg3_rank_shard_full_size():
+    L = _L()
+    per, rank = 125000, 3
+    byz = list(range(11, 16))
+    kw = dict(n=16, f=5, protocol="consensus", seed=0x5EED0003, delay_model=L.DELAY_UNIFORM, delay_max=4,
+              round_cap=1, step_cap=4000, key_window=4, variants=2, proposals=L.PROPOSALS_PHILOX,
+              byz_pattern=L.BYZ_EQUIVOCATE, byzantine=byz)
+    first = rank * per
+    ids = random.Random(3).sample(range(per), 24)
+    res, reps = _run(kw, first, per, ids)
+    assert not any(r["status"] in ("overflow", "bad_injection", "running") for r in res)
+    make = lambda g: S.cons_spec(16, 5, 0x5EED0003, 1, 4, g, round_cap=1, byzantine=byz, nv=2,  # noqa: E731
+                                 extra=S.equivocation_actions(16, byz))
+    _check_sample(res, reps, kw, first, ids, make)
+    _sharding_invariant(kw, first, per, res)
+
+
+@pytest.mark.parametrize("mode", ["reference", "spec"])
+def test_cfg4_bench_batch_full_size(mode):
+    L = _L()
+    N = 131072
+    spec = mode == "spec"
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=1, step_cap=4000, key_window=8 if spec else 4, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        res = eng.instances_result()
+        hist = eng.round_histogram(66)
+        reps = eng.replicas(0, 8) + eng.replicas(N - 8, 8)
+    assert hist[0] == 0 and sum(hist) == N, "every instance decided"
+    if spec:
+        make = lambda g: S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1, window=8,  # noqa: E731
+                                          coin_seed=0xC017C017)
+    else:
+        make = lambda g: S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1)  # noqa: E731
+    sub = res[:8] + res[N - 8:]
+    ids = list(range(8)) + list(range(N - 8, N))
+    for j, g in enumerate(ids):
+        exp = oracle.run(make(g))
+        for k in KEYS:
+            assert sub[j][k] == exp[k], (g, k)
+        first = {}
+        for t, node, rnd, val in sorted(exp["events"]["decide"]):
+            first.setdefault(node, rnd)
+        assert [r["first_decide_round"] for r in reps[j]] == [first[d] for d in range(64)]
+
+
+@pytest.mark.parametrize("model,dmax", [(0, 1), (1, 4), (3, 16)])
+def test_cfg5_n256_full_size(model, dmax):
+    L = _L()
+    N = 512
+    kw = dict(n=256, f=85, protocol="consensus", seed=0x5EED0005, delay_model=model, delay_max=dmax,
+              round_cap=1, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC,
+              coin_seed=0xC017C017)
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        res = eng.instances_result()
+        hist = eng.round_histogram(66)
+    assert hist[0] == 0 and sum(hist) == N
+    assert all(r["status"] == "done" for r in res)
+    if model != 0:
+        return
+    g = N - 1   # one instance vs the oracle (an n = 256 oracle run takes about a minute)
+    exp = oracle.run(S.spec_cons_spec(256, 85, 0x5EED0005, model, dmax, g, round_cap=1, window=8,
+                                      coin_seed=0xC017C017))
+    for k in KEYS:
+        assert res[g][k] == exp[k], (g, k)

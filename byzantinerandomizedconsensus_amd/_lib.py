@@ -81,7 +81,7 @@ class ReplicaResult(ctypes.Structure):
 
 class Event(ctypes.Structure):
     _fields_ = [("instance", ctypes.c_uint64), ("t", ctypes.c_uint32), ("kind", ctypes.c_uint8),
-                ("node", ctypes.c_uint8), ("type", ctypes.c_uint8), ("pad", ctypes.c_uint8),
+                ("node", ctypes.c_uint8), ("type", ctypes.c_uint8), ("value", ctypes.c_uint8),
                 ("a", ctypes.c_uint32), ("b", ctypes.c_uint32)]
 
 

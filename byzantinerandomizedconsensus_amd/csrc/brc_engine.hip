@@ -112,6 +112,7 @@ struct Engine {
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
+    uint32_t rows = 0;                           // cell rows per item
     uint64_t cons_bytes = 0;                     // consensus-set buffer (hmask) bytes per item
     uint64_t nitems = 0;
     hipStream_t stream = nullptr;
@@ -185,7 +186,7 @@ static void free_all(Engine* e) {
 }
 
 static int clear_state(Engine* e, bool full) {
-    const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
+    const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
     const size_t keys = (size_t)e->cfg.instances * e->NK;
     if (full) {
         const uint64_t fb = std::min<uint64_t>((cells + 255) / 256, 1u << 20);
@@ -313,6 +314,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->bw = e->wide ? (uint32_t)e->npad / 64 : 1u;
     e->nkw_t = e->npad / 8 < 1 ? 1 : e->npad / 8;
     e->NK = (uint32_t)e->npad * c.variants * c.key_window;
+    e->rows = e->wide ? e->NK : e->NK + 1;       // narrow kernel: + the trash row (brc_step.h)
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
@@ -334,7 +336,7 @@ int brc_create(const brc_config* cfg, void** out) {
     if (hipSetDevice(c.device) != hipSuccess) { g_create_err = "hipSetDevice failed"; delete e; return BRC_E_HIP; }
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail(BRC_E_HIP);
     if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) return fail(BRC_E_HIP);
-    const size_t cells = (size_t)e->nitems * e->NK * e->lpi;
+    const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, cells * 8}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},

@@ -22,7 +22,9 @@
 // A cell whose generation differs from its key slot's is stale in every field, send steps
 // included, so recycling a slot (or a whole batch, brc_reset) never touches the cells.
 // HBM (lane-contiguous => every access is one coalesced 512-B wave access):
-//   cells [item][NK][64] u64
+//   cells [item][NK + 1][64] u64 -- row NK is a trash row: the key loop runs whole chunks, and the
+//   padding slots of the last chunk load and store it, so no load or store is conditional and the
+//   compiler can wait for exactly the loads a chunk needs while the next chunk's are in flight
 // per instance key slots (copied to LDS for the launch): meta [inst][NK] u64 (s+1 | t_send |
 //   t_quiet | sender | value), mgen [inst][NK] u32 (generation | restricted-SEND flag),
 //   kdst [inst][NK] u64 (SEND destinations, read only for restricted SENDs)
@@ -34,10 +36,6 @@
 
 namespace brc {
 
-#ifndef BRC_CHUNK
-#define BRC_CHUNK 4
-#endif
-constexpr int CHUNK = BRC_CHUNK;  // key slots whose cell loads are in flight together
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
 
 template <int NPAD> struct MaskOf { using type = uint64_t; };
@@ -300,7 +298,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
-    const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)NK * 64 + lane;   // cell (k, lane) at [k * 64]
+    const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64 + lane;   // cell (k, lane) at [k * 64]
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
@@ -324,13 +322,13 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
 
     uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
 
-    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b) {
+    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b, uint32_t v) {
         if (EV) {
             const unsigned long long i = atomicAdd(P.event_count, 1ull);
             if (i < P.event_cap) {
                 brc_event e;
                 e.instance = inst; e.t = t; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
-                e.type = (uint8_t)type; e.pad = 0; e.a = a; e.b = b;
+                e.type = (uint8_t)type; e.value = (uint8_t)v; e.a = a; e.b = b;
                 P.events[i] = e;
             }
         }
@@ -356,7 +354,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         q_until = max(q_until, t + maxout);
         st_msgs += n;
         st_smax = max(st_smax, s);
-        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
+        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s, v);
     };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
@@ -387,7 +385,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             ++dcount;
             if (dcount == 1) { frnd = round; ft = t; fval = dec; }
             lval = dec;
-            log_ev(BRC_EV_DECIDE, d, 0, round, dec);
+            log_ev(BRC_EV_DECIDE, d, 0, round, dec, dec);
             ++round; phase = 1; cons_reset();                        // :96-100
             send_key(2 * (round - 1), dec);                          // :102-106
         }
@@ -417,7 +415,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                     ++dcount;
                     if (dcount == 1) { frnd = round; ft = t; fval = vmax; }
                     lval = vmax;
-                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax);
+                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax, vmax);
                     est = vmax;
                 } else if (cmax > P.f) {
                     est = vmax;
@@ -500,7 +498,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                                 gp(P.kdst)[inst * NK + k] = r.dst;
                                 mark_lane(k, os);
                                 st_msgs += __popcll(r.dst & all64);
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s, (uint32_t)(uint8_t)r.value);
                             }
                         }
                     }
@@ -515,8 +513,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                         badinj = true;
                     } else {
                         const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
-                        const size_t ci = ((size_t)item * NK + k) * 64 + lane;
-                        uint64_t wv = gp(P.cells)[ci];
+                        uint64_t wv = mycells[(size_t)k * 64];
                         if (((wv >> 19) & GEN_MASK) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 19);
                         const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
                         if (!(wv & bit)) {
@@ -524,9 +521,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                             wv |= bit;
                             const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            gp(P.cells)[ci] = wv;
+                            mycells[(size_t)k * 64] = wv;
                             st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
+                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
                         }
                     }
                 }
@@ -584,20 +581,20 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             if ((bits >> lane) & 1) s_klist[nkeys + below] = w * 64 + lane;
             nkeys += (uint32_t)__popcll(bits);
         }
+        if (lane < 2 * CHUNK) s_klist[nkeys + lane] = NK;   // chunk padding -> the trash row
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {
+        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {     // p < nkeys + CHUNK: padded list
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
-                ww[c] = TIMES_NEVER;
-                if (p + c < nkeys) ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * 64];
+                ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * 64];
             });
         };
         auto process = [&](const uint32_t k, const uint64_t wd) {
-            uint64_t m = s_meta[mbase + k];
+            uint64_t m = s_meta[mbase + k];                      // (k == NK, the trash row: junk, unused)
             uint32_t gw = s_gen[mbase + k];
             if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
             const uint32_t gen = gw & GEN_MASK;
-            const bool kl = m_s1(m) != 0;                        // the slot holds a key
+            const bool kl = k < NK && m_s1(m) != 0;              // the slot holds a key
             const bool live = kl && running;
             const bool cur = kl && real_run && (((uint32_t)wd >> 19) & GEN_MASK) == gen;
             const uint64_t word = cur ? wd : TIMES_NEVER;
@@ -647,9 +644,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
             if (EV) {
                 const uint32_t kp = k / Q, s = m_s1(m) - 1u;
-                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
-                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
-                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
+                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends: ring marks at t + every delay some sending lane has; t_quiet of the key
             const uint64_t sb = __ballot(es || rs);
@@ -682,7 +679,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 fetch(p + CHUNK, wB);
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    if (p + c < nkeys) process(uni32(s_klist[p + c]), wA[c]);
+                    process(uni32(s_klist[p + c]), wA[c]);       // padding slots: the trash row
                 });
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;

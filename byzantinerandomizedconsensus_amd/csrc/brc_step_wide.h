@@ -243,13 +243,13 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         return x;
     };
 
-    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b) {
+    auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b, uint32_t v) {
         if (EV) {
             const unsigned long long i = atomicAdd(P.event_count, 1ull);
             if (i < P.event_cap) {
                 brc_event e;
                 e.instance = inst; e.t = t; e.kind = (uint8_t)kind; e.node = (uint8_t)node;
-                e.type = (uint8_t)type; e.pad = 0; e.a = a; e.b = b;
+                e.type = (uint8_t)type; e.value = (uint8_t)v; e.a = a; e.b = b;
                 P.events[i] = e;
             }
         }
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         q_until = max(q_until, t + maxout);
         st_msgs += n;
         st_smax = max(st_smax, s);
-        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s);
+        log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s, v);
     };
     auto popc_hm = [&](uint32_t v) -> uint32_t {
         uint32_t c = 0;
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             ++dcount;                                                // :89 never equal -> :94
             if (dcount == 1) { frnd = round; ft = t; fval = dec; }
             lval = dec;
-            log_ev(BRC_EV_DECIDE, d, 0, round, dec);
+            log_ev(BRC_EV_DECIDE, d, 0, round, dec, dec);
             ++round; phase = 1; cons_reset();                        // :96-100
             send_key(2 * (round - 1), dec);                          // :102-106
         }
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                     ++dcount;
                     if (dcount == 1) { frnd = round; ft = t; fval = vmax; }
                     lval = vmax;
-                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax);
+                    log_ev(BRC_EV_DECIDE, d, 0, round, vmax, vmax);
                     est = vmax;
                 } else if (cmax > P.f) {
                     est = vmax;
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                             if (is_send) {
                                 mark_lane(k, os);
                                 st_msgs += n;
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s);
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s, (uint32_t)(uint8_t)r.value);
                             }
                         }
                     }
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                             mycells[(size_t)k * NPAD] = wv;
                             st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s);
+                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
                         }
                     }
                 }
@@ -562,9 +562,9 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             if (dl) s_dbits[(k >> 6) * NPAD + d] |= 1ull << (k & 63);
             if (EV) {
                 const uint32_t kp = k / Q, s = m_s1(m) - 1u;
-                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s);
-                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s);
-                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s);
+                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
             const uint64_t sb = __ballot(es || rs);

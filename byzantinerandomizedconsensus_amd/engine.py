@@ -135,6 +135,7 @@ class Engine:
         return out
 
     def events(self):
+        """Event log: (instance, t, kind, node, type, a, b, value id) tuples, in device order."""
         cnt = ctypes.c_size_t(0)
         self._chk(self._lib.brc_read_events(self._h, None, 0, ctypes.byref(cnt)))
         cap = min(cnt.value, self.cfg.event_capacity)
@@ -143,7 +144,7 @@ class Engine:
         if cnt.value > self.cfg.event_capacity:
             raise L.EngineError(L.E_STATE, "event log overflow: %d events, capacity %d"
                                 % (cnt.value, self.cfg.event_capacity))
-        return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b) for e in arr[:cap]]
+        return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b, e.value) for e in arr[:cap]]
 
     def round_histogram(self, bins=66):
         """hist[r] = instances whose honest replicas had all decided by round r; hist[0] =

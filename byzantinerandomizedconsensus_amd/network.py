@@ -239,7 +239,7 @@ class Cluster:
         evs = self.engine.events()
         new, self.seen_events = evs[self.seen_events:], len(evs)
         by_t = {}
-        for (_inst, t, kind, node, _typ, a, b) in new:
+        for (_inst, t, kind, node, _typ, a, b, _v) in new:
             if kind in (L.EV_DELIVER, L.EV_DECIDE):
                 by_t.setdefault(t, []).append((kind, node, a, b))
         for t in sorted(by_t):

@@ -118,7 +118,8 @@ typedef struct {
 typedef struct {
     uint64_t instance;
     uint32_t t;
-    uint8_t kind, node, type, pad;
+    uint8_t kind, node, type;
+    uint8_t value;            /* value id of the key's payload (DECIDE: the decided value) */
     uint32_t a, b;            /* DELIVER: kp, s   DECIDE: round, value   SEND: kp, s */
 } brc_event;
 

@@ -82,7 +82,7 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
     finally:
         eng.close()
     per = [{"deliver": [], "decide": [], "send": []} for _ in specs]
-    for (inst, t, kind, node, typ, a, b) in evs:
+    for (inst, t, kind, node, typ, a, b, _v) in evs:
         if kind == L.EV_DELIVER:
             per[inst]["deliver"].append([t, node, a, b])
         elif kind == L.EV_DECIDE:

@@ -81,10 +81,31 @@ def fuzz_specs(count, rng):
     return out
 
 
+def wire_specs():
+    """Small runs whose every wire message (the bytes base/broadcast.py:37-38 puts on a TCP
+    connection) is kept: BRB, consensus, and a Byzantine equivocator."""
+    G = S.scenario_groups()
+    return [G["brb_fifo_n4"][0], G["cons_brc_test_n6"][0], G["cons_uniform_n4"][0], G["brb_byz_n7"][0]]
+
+
+def write_wire():
+    cases = []
+    for sp in wire_specs():
+        ref = run_spec(sp, Schedule)
+        wire = sorted(ref["wire"])
+        cases.append({"spec": sp, "wire": wire, "result": compact(ref)})
+        print("%-24s %6d wire messages" % (sp["name"], len(wire)))
+    with open(os.path.join(HERE, "wire.json"), "w") as fh:
+        json.dump({"group": "wire", "generator": "tests/golden/make_golden.py --wire",
+                   "source": "unmodified reference classes via tests/golden/refharness.py; addresses "
+                             "('localhost', 7000 + node)", "cases": cases}, fh, separators=(",", ":"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fuzz", type=int, default=0)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--wire", action="store_true", help="write tests/golden/wire.json (SURVEY F2)")
     args = ap.parse_args()
     if __debug__:
         sys.exit("run with python -O (the reference asserts N > 5f)")
@@ -100,6 +121,9 @@ def main():
                 print("MISMATCH", sp["name"], json.dumps(sp)[:300])
         print("fuzz: %d specs, %d mismatches, %.1fs" % (args.fuzz, bad, time.time() - t0))
         sys.exit(1 if bad else 0)
+    if args.wire:
+        write_wire()
+        return
     groups = S.scenario_groups()
     for name, specs in groups.items():
         if args.only and name != args.only:

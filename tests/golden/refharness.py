@@ -39,6 +39,7 @@ class HarnessError(RuntimeError):
 
 
 def _import_reference():
+    sys.dont_write_bytecode = True     # the reference tree is read-only: no __pycache__ there
     if REFERENCE not in sys.path:
         sys.path.insert(0, REFERENCE)
     import byzantinerandomizedconsensus.base.broadcast as bmod
@@ -194,6 +195,7 @@ class Run:
         self.key_of_payload = {}
         self.payload_of_key = {}
         self.events = {"deliver": [], "decide": [], "send": []}
+        self.wire = []                  # [t, src, dst, envelope] of every message the network carries
         self.msgs_sent = 0
         self.arrivals_processed = 0
         self.last_active = 0
@@ -238,6 +240,7 @@ class Run:
             return
         self.sent.add(ident)
         self.msgs_sent += 1
+        self.wire.append([self.t, src, dst, data.decode("utf-8")])
         fs = (src, mtype, payload)
         if fs not in self.first_sends:
             self.first_sends.add(fs)
@@ -383,6 +386,7 @@ class Run:
             "msgs_sent": self.msgs_sent,
             "arrivals": self.arrivals_processed,
             "events": self.events,
+            "wire": self.wire,
         }
 
 

@@ -161,16 +161,16 @@ static uint64_t word_mask(uint32_t n, uint32_t w) {
 
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
-static int launch_step(int npad, int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t st,
+static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t st,
                        const Params* P) {
     switch (npad) {
-    case 4: return launch_step_4(dm, events, spec, blocks, lds, st, P);
-    case 8: return launch_step_8(dm, events, spec, blocks, lds, st, P);
-    case 16: return launch_step_16(dm, events, spec, blocks, lds, st, P);
-    case 32: return launch_step_32(dm, events, spec, blocks, lds, st, P);
-    case 64: return launch_step_64(dm, events, spec, blocks, lds, st, P);
-    case 128: return launch_step_128(dm, events, spec, blocks, lds, st, P);
-    case 256: return launch_step_256(dm, events, spec, blocks, lds, st, P);
+    case 4: return launch_step_4(dm, events, mode, blocks, lds, st, P);
+    case 8: return launch_step_8(dm, events, mode, blocks, lds, st, P);
+    case 16: return launch_step_16(dm, events, mode, blocks, lds, st, P);
+    case 32: return launch_step_32(dm, events, mode, blocks, lds, st, P);
+    case 64: return launch_step_64(dm, events, mode, blocks, lds, st, P);
+    case 128: return launch_step_128(dm, events, mode, blocks, lds, st, P);
+    case 256: return launch_step_256(dm, events, mode, blocks, lds, st, P);
     default: return BRC_E_INVALID;
     }
 }
@@ -298,7 +298,7 @@ int brc_create(const brc_config* cfg, void** out) {
         !(c.variants == 1 || c.variants == 2 || c.variants == 4) || c.key_window * c.variants > 8 ||
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
-        c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_SPEC ||
+        c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB ||
         (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE) || (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
     {
         g_create_err = "invalid configuration (see include/brc.h field ranges)";
@@ -511,7 +511,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
-    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, c.mode == BRC_MODE_SPEC, blocks, e->lds_bytes, e->stream,
+    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, (int)c.mode, blocks, e->lds_bytes, e->stream,
                      e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }

@@ -107,13 +107,13 @@ inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
-int launch_step_4(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_8(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_16(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_32(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_64(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_4(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_8(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_16(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_32(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_64(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 // wide kernel (brc_step_wide.h): one workgroup of NPAD threads per instance
-int launch_step_128(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_256(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_128(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_256(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 
 }  // namespace brc

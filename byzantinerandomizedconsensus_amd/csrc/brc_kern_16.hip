@@ -3,7 +3,7 @@
 #include "brc_step.h"
 
 namespace brc {
-int launch_step_16(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    return launch_step<16>(dm, events, spec, blocks, lds, s, P);
+int launch_step_16(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    return launch_step<16>(dm, events, mode, blocks, lds, s, P);
 }
 }  // namespace brc

@@ -171,16 +171,27 @@ __device__ __forceinline__ void brb_cell_update_spec(uint32_t& fl, uint32_t& ec,
     fl |= deliver ? F_DEL : 0u;
 }
 
+// Best-effort broadcast (BRC_MODE_BEB; core/bebroadcast.py:30-42 as intended -- its constructor
+// raises TypeError): a SEND delivers at its arrival, nothing is echoed.  The network suppresses
+// duplicates, so each (origin, key) SEND reaches a receiver once.
+__device__ __forceinline__ void brb_cell_update_beb(uint32_t& fl, bool s_arr, bool& echo_send, bool& ready_send,
+                                                    bool& deliver) {
+    deliver = s_arr && !(fl & F_DEL);
+    fl |= deliver ? F_DEL : 0u;
+    echo_send = ready_send = false;
+}
+
 #ifndef BRC_MIN_WAVES
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
 
-template <int NPAD, int DM, bool EV, bool SPEC>
+template <int NPAD, int DM, bool EV, int MODE>
 __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params* pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
     // pinning ~60 of them in SGPRs across the hot loop.  Hot fields are copied to locals below.
     const Params& P = *pp;
+    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
     using T = typename MaskOf<NPAD>::type;
     constexpr int IPW = 64 / NPAD;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -628,7 +639,8 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             st_loads += (kl && real_run) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
             bool es, rs, dl;
-            if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
+            else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {   // whole-wave store (lanes without arrivals write their word back unchanged)
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
@@ -814,9 +826,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
 }
 
 // Launch one (DM, EV, SPEC) instantiation of the step kernel for a fixed NPAD.
-template <int NPAD, int DMX, bool EV, bool SPEC>
+template <int NPAD, int DMX, bool EV, int MODE>
 int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step<NPAD, DMX, EV, SPEC>;
+    auto kern = brc_step<NPAD, DMX, EV, MODE>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -825,13 +837,12 @@ int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 }
 
 template <int NPAD>
-int launch_step(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
-        if (spec) return events ? launch_one<NPAD, DMX, true, true>(blocks, lds, s, P)                 \
-                                : launch_one<NPAD, DMX, false, true>(blocks, lds, s, P);               \
-        return events ? launch_one<NPAD, DMX, true, false>(blocks, lds, s, P)                          \
-                      : launch_one<NPAD, DMX, false, false>(blocks, lds, s, P);                        \
+        if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \
+        if (mode == BRC_MODE_BEB) return events ? launch_one<NPAD, DMX, true, BRC_MODE_BEB>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_BEB>(blocks, lds, s, P); \
+        return events ? launch_one<NPAD, DMX, true, BRC_MODE_REFERENCE>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_REFERENCE>(blocks, lds, s, P); \
     }
 #ifdef BRC_ONLY_DM8
     BRC_CASE(8)

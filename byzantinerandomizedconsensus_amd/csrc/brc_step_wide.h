@@ -41,9 +41,10 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return x;
 }
 
-template <int NPAD, int DM, bool EV, bool SPEC>
+template <int NPAD, int DM, bool EV, int MODE>
 __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const Params& P = *pp;
+    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
     constexpr int NW = NPAD / 64;
     constexpr int NPL = DM == 4 ? 2 : DM == 8 ? 3 : 4;   // bit planes of a link's delay code
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -547,7 +548,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             st_loads += (kl && real) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 255, rc = (uint32_t)(word >> 13) & 255;
             bool es, rs, dl;
-            if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
+            else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
@@ -704,9 +706,9 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     }
 }
 
-template <int NPAD, int DMX, bool EV, bool SPEC>
+template <int NPAD, int DMX, bool EV, int MODE>
 int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step_wide<NPAD, DMX, EV, SPEC>;
+    auto kern = brc_step_wide<NPAD, DMX, EV, MODE>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -715,13 +717,12 @@ int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* 
 }
 
 template <int NPAD>
-int launch_step_wide(int dm, bool events, bool spec, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+int launch_step_wide(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
-        if (spec) return events ? launch_wide_one<NPAD, DMX, true, true>(blocks, lds, s, P)            \
-                                : launch_wide_one<NPAD, DMX, false, true>(blocks, lds, s, P);          \
-        return events ? launch_wide_one<NPAD, DMX, true, false>(blocks, lds, s, P)                     \
-                      : launch_wide_one<NPAD, DMX, false, false>(blocks, lds, s, P);                   \
+        if (mode == BRC_MODE_SPEC) return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \
+        if (mode == BRC_MODE_BEB) return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_BEB>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_BEB>(blocks, lds, s, P); \
+        return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_REFERENCE>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_REFERENCE>(blocks, lds, s, P); \
     }
     BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
 #undef BRC_CASE

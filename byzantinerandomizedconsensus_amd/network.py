@@ -138,6 +138,7 @@ class Cluster:
         self.seen_events = 0
         self.finished = False
         self.status = None
+        self.beb = False           # best-effort broadcast nodes (core/bebroadcast.py)
 
     # ------------------------------------------------------------------ registration
     def node_id(self, host):
@@ -150,10 +151,24 @@ class Cluster:
         i = self.node_id(node.host)
         if self.engine is not None:
             raise L.EngineError(L.E_STATE, "node added after the cluster started running")
+        if self.beb:
+            raise ValueError("BEBroadcast and BRBroadcast nodes cannot share a peer list")
         if self.N is None:
             self.N, self.f = N, f
         elif (self.N, self.f) != (N, f):
             raise ValueError("nodes of one peer list disagree on (N, f)")
+        self.nodes[i] = node
+        return i
+
+    def add_beb(self, node):
+        """A best-effort broadcast node (core/bebroadcast.py): no thresholds, f = 0."""
+        i = self.node_id(node.host)
+        if self.engine is not None:
+            raise L.EngineError(L.E_STATE, "node added after the cluster started running")
+        if self.N is not None and not self.beb:
+            raise ValueError("BEBroadcast and BRBroadcast nodes cannot share a peer list")
+        self.beb = True
+        self.N, self.f = len(self.peers), 0
         self.nodes[i] = node
         return i
 
@@ -203,7 +218,7 @@ class Cluster:
                              round_cap=c["round_cap"] if self.cons else 0, step_cap=c["step_cap"],
                              key_window=8, variants=1, byzantine=silent,
                              event_capacity=c["event_capacity"], instance_offset=c["instance_id"],
-                             device=c["device"])
+                             device=c["device"], mode=L.MODE_BEB if self.beb else L.MODE_REFERENCE)
 
     def _flush(self):
         if self.actions:

@@ -49,7 +49,10 @@ enum { BRC_PROTO_BRB = 0, BRC_PROTO_CONSENSUS = 1 };
  * K1-K12).  BRC_MODE_SPEC: the protocol the reference intends (Bracha-correct broadcast; consensus
  * with per-phase windows and the core/byzantinerandomizedconsensus.py:88-92 coin made reachable as
  * a common Philox coin keyed (coin_seed, instance, round)). */
-enum { BRC_MODE_REFERENCE = 0, BRC_MODE_SPEC = 1 };
+/* BRC_MODE_BEB: best-effort broadcast (core/bebroadcast.py as intended -- the reference's class
+ * cannot be constructed): a SEND delivers at its arrival, no ECHO/READY; with BRC_PROTO_CONSENSUS
+ * the reference's consensus runs on top of it (its consensus_instance.deliver, :42). */
+enum { BRC_MODE_REFERENCE = 0, BRC_MODE_SPEC = 1, BRC_MODE_BEB = 2 };
 enum { BRC_PEER_SENDER = 0 };
 enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DELAY_GEOMETRIC = 3 };
 enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };

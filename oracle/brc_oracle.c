@@ -360,6 +360,21 @@ static void brb_on_message_spec(sim_t* S, const msg_t* m) {
     }
 }
 
+/* core/bebroadcast.py:30-42 as intended (its constructor passes the wrong arguments to
+ * Broadcast.__init__ and raises): every received message is delivered -- to the consensus
+ * instance in BEB_CONSENSUS mode (:42).  Only SENDs are ever sent; the network delivers each
+ * (origin, key) SEND once. */
+static void beb_on_message(sim_t* S, const msg_t* m) {
+    key_t_* k = &S->keys[m->key];
+    cell_t* c = &k->cells[m->dst];
+    S->res->arrivals++;
+    if (m->type != OR_SEND || c->del) return;
+    c->del = 1;
+    uint32_t ev[4] = {S->t, m->dst, k->kp, k->s};
+    push_event(S->res->deliver, S->res->deliver_cap, &S->res->n_deliver, 4, ev);
+    if (S->sp->mode == OR_MODE_BEB_CONSENSUS) cons_deliver(S, m->dst, (int)m->key);
+}
+
 /* core/brbroadcast.py:60-119, one accept-loop iteration at node `dst`; the peer address is
  * the sender id (sender-identity mode, :71). */
 static void brb_on_message(sim_t* S, const msg_t* m) {
@@ -474,14 +489,17 @@ int oracle_run(const oracle_spec* sp, oracle_result* res) {
         b->v = NULL; b->n = 0; b->cap = 0;
         qsort(v, cnt, sizeof(msg_t), msg_cmp);
         const int spec = sp->mode == OR_MODE_SPEC || sp->mode == OR_MODE_SPEC_BRB;
+        const int beb = sp->mode == OR_MODE_BEB || sp->mode == OR_MODE_BEB_CONSENSUS;
         for (size_t i = 0; i < cnt && !S->err; ++i) {
             if (spec) brb_on_message_spec(S, &v[i]);
+            else if (beb) beb_on_message(S, &v[i]);
             else brb_on_message(S, &v[i]);
         }
         free(v);
         while (ai < sp->n_actions && sp->actions[ai].t == nt) do_action(S, &sp->actions[ai++]);
         if (S->overflow) { res->status = OR_ST_OVERFLOW; break; }
-        if ((sp->mode == OR_MODE_CONSENSUS || sp->mode == OR_MODE_SPEC) && sp->round_cap > 0) {
+        if ((sp->mode == OR_MODE_CONSENSUS || sp->mode == OR_MODE_SPEC || sp->mode == OR_MODE_BEB_CONSENSUS) &&
+            sp->round_cap > 0) {
             int all = 1;
             for (uint32_t i = 0; i < S->n; ++i)
                 if (is_honest(S, i) && S->cons[i].decides < sp->round_cap) { all = 0; break; }

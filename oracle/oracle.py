@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 ACT = {"propose": 1, "brb_send": 2, "byz_key": 3, "byz": 4}
 STATUS = {1: "done", 2: "quiescent", 3: "stepcap", 4: "overflow"}
-MODES = {"brb": 0, "consensus": 1, "spec": 2, "spec_brb": 3}
+MODES = {"brb": 0, "consensus": 1, "spec": 2, "spec_brb": 3, "beb": 4, "beb_consensus": 5}
 
 
 class _Action(ctypes.Structure):

@@ -64,12 +64,14 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
         key_window = sp0["window"]          # the SPEC buffering window IS the engine's key window
     elif key_window is None:
         key_window = 8 // sp0.get("nv", 1)
-    protocol = {"spec": "consensus", "spec_brb": "brb"}.get(sp0["mode"], sp0["mode"])
+    protocol = {"spec": "consensus", "spec_brb": "brb", "beb": "brb", "beb_consensus": "consensus"}.get(
+        sp0["mode"], sp0["mode"])
+    mode = L.MODE_SPEC if spec_mode else (L.MODE_BEB if sp0["mode"].startswith("beb") else L.MODE_REFERENCE)
     eng = Engine(n=sp0["n"], f=sp0["f"], instances=len(specs), protocol=protocol, seed=sp0["seed"],
                  delay_model=sp0["delay_model"], delay_max=sp0["dmax"], delay_const=sp0.get("dconst", 1),
                  round_cap=sp0.get("round_cap", 0), step_cap=sp0.get("step_cap", 10000), key_window=key_window,
                  variants=sp0.get("nv", 1), byzantine=sp0.get("byzantine", ()), event_capacity=event_capacity,
-                 instance_offset=sp0["g"], device=device, mode=L.MODE_SPEC if spec_mode else L.MODE_REFERENCE,
+                 instance_offset=sp0["g"], device=device, mode=mode,
                  coin_seed=sp0.get("coin_seed", 0))
     try:
         inj = []

@@ -66,6 +66,20 @@ def spec_brb_spec(n, f, seed, model, dmax, g, sends, window=4, **kw):
     return sp
 
 
+def beb_spec(n, seed, model, dmax, g, sends, **kw):
+    """Best-effort broadcast only (core/bebroadcast.py as intended; BRC_MODE_BEB)."""
+    sp = brb_spec(n, 0, seed, model, dmax, g, sends, **kw)
+    sp.update(mode="beb")
+    return sp
+
+
+def beb_cons_spec(n, f, seed, model, dmax, g, round_cap=1, **kw):
+    """The reference's consensus over best-effort broadcast (its consensus_instance.deliver)."""
+    sp = cons_spec(n, f, seed, model, dmax, g, round_cap=round_cap, **kw)
+    sp.update(mode="beb_consensus")
+    return sp
+
+
 def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
     """SURVEY §8(d) cfg3 pattern: each Byzantine replica b SENDs value "0" to even
     destinations and "1" to odd ones, then ECHOes and READYs both keys to everyone."""

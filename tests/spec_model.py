@@ -1,4 +1,5 @@
-"""Independent pure-Python model of the SPEC protocol modes (TEST INFRASTRUCTURE ONLY).
+"""Independent pure-Python model of the SPEC protocol modes and of best-effort broadcast
+(TEST INFRASTRUCTURE ONLY).
 
 The reference never runs the protocol it intends: its broadcast echoes on an ECHO-created entry
 (core/brbroadcast.py:76-98) and its consensus coin branch is dead (:89-92 of
@@ -30,8 +31,8 @@ def coin_id(coin_seed, g, rnd):
 
 def run(spec):
     n, f, nv = spec["n"], spec["f"], spec.get("nv", 1)
-    mode, window, g = spec["mode"], spec["window"], spec["g"]
-    assert mode in ("spec", "spec_brb")
+    mode, window, g = spec["mode"], spec.get("window", 4), spec["g"]
+    assert mode in ("spec", "spec_brb", "beb")
     sch = Schedule(n, f, spec["seed"], spec["delay_model"], spec["dmax"], spec.get("dconst", 1))
     byz = set(spec.get("byzantine", []))
     values = spec.get("values")
@@ -116,6 +117,11 @@ def run(spec):
         st["arrivals"] += 1
         c = cells.setdefault((dst, kp, s), {"E": set(), "R": set(), "es": False, "rs": False, "dl": False})
         if c["dl"]:
+            return
+        if mode == "beb":               # best-effort broadcast: a SEND delivers, nothing is echoed
+            if typ == SEND:
+                c["dl"] = True
+                ev["deliver"].append([st["t"], dst, kp, s])
             return
         if typ == SEND:
             if not c["es"]:

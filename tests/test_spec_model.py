@@ -69,3 +69,20 @@ def test_spec_coin_rounds_happen():
         assert len({d[3] for d in dec}) == 1, "agreement"
         seen_coin |= max(d[2] for d in dec) > 1
     assert seen_coin, "no instance needed a coin round"
+
+
+def test_oracle_beb_matches_model():
+    """Best-effort broadcast: the C oracle's beb_on_message against the model."""
+    rng = random.Random(44)
+    for i in range(60):
+        n = rng.choice([3, 4, 7, 10, 16])
+        model = rng.randint(0, 3)
+        dmax = rng.randint(1, 6) if model else 1
+        sends = [(rng.randint(0, 6), o, q) for o in range(n) for q in range(rng.randint(0, 2))]
+        byz = rng.sample(range(n), rng.randint(0, n // 3))
+        sp = S.beb_spec(n, rng.getrandbits(40), model, dmax, rng.getrandbits(20),
+                        [x for x in sends if x[1] not in byz], byzantine=byz)
+        sp["name"] = "beb/%d" % i
+        r = _check(sp)
+        honest = n - len(byz)
+        assert len(r["events"]["deliver"]) == honest * len([x for x in sends if x[1] not in byz])

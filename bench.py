@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--instances", type=int, default=1 << 17, help="instances per GPU")
+    ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
     ap.add_argument("--key-window", type=int, default=0, help="0: 4 (reference mode), 8 (spec mode)")
     ap.add_argument("--mode", choices=("reference", "spec"), default="reference",
                     help="reference: the protocol as the reference runs it (headline); spec: the intended "

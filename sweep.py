@@ -25,6 +25,7 @@ N = 256
 SEED, COIN_SEED = 0x5EED0005, 0xC017C017
 MODELS = {"const": (0, 1), "uniform": (1, 4), "geometric": (3, 16)}   # (BRC_DELAY_*, delay_max)
 BINS = 66
+BYTES_PER_CELL_STEP = 6 * ((N + 7) // 8) + 2      # 194 B at n = 256
 
 
 def parse():
@@ -84,6 +85,10 @@ def main():
                                                                        "running")},
                     "round_hist": {str(r): c for r, c in enumerate(hist) if c}, "mean_decide_round": mean_r,
                     "max_decide_round": last, "msgs_sent": st["msgs_sent"], "arrivals": st["arrivals"],
+                    "cell_steps": st["cell_steps"],
+                    "roofline": {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,
+                                 "achieved": BYTES_PER_CELL_STEP * st["cell_steps"] / world / (kms / 1e3) / 1e9,
+                                 "note": "algorithmic %d B per cell-step (SURVEY 8(d) at n=256)" % BYTES_PER_CELL_STEP},
                     "kernel_ms": kms, "wall_ms": wall * 1e3, "setup_ms": (t1 - t0) * 1e3,
                     "decided_instances_per_s": decided / wall if wall else None}), flush=True)
     if dist is not None:

@@ -18,7 +18,7 @@ ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP e
 
 PROTO_BRB, PROTO_CONSENSUS = 0, 1
 MODE_REFERENCE, MODE_SPEC, MODE_BEB = 0, 1, 2
-PEER_SENDER = 0
+PEER_SENDER, PEER_CONNECTION = 0, 1
 DELAY_CONST, DELAY_UNIFORM, DELAY_SLOWSET, DELAY_GEOMETRIC = 0, 1, 2, 3
 PROPOSALS_NONE, PROPOSALS_PHILOX, PROPOSALS_LOADED = 0, 1, 2
 BYZ_NONE, BYZ_EQUIVOCATE = 0, 1

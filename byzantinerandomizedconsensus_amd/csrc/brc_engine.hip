@@ -291,7 +291,8 @@ int brc_create(const brc_config* cfg, void** out) {
     *out = nullptr;
     const brc_config& c = *cfg;
     if (c.n < 1 || c.n > 256 || c.instances == 0 || c.delay_max < 1 || c.delay_max > 16 ||
-        c.step_cap > STEP_LIMIT || c.peer_mode != BRC_PEER_SENDER ||
+        c.step_cap > STEP_LIMIT || c.peer_mode > BRC_PEER_CONNECTION ||
+        (c.peer_mode == BRC_PEER_CONNECTION && (c.mode != BRC_MODE_REFERENCE || c.n > 64 || c.delay_max > 8)) ||
         (c.protocol != BRC_PROTO_BRB && c.protocol != BRC_PROTO_CONSENSUS) || c.delay_model > BRC_DELAY_GEOMETRIC ||
         (c.delay_model == BRC_DELAY_CONST && (c.delay_const < 1 || c.delay_const > c.delay_max)) ||
         !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8) ||
@@ -314,7 +315,8 @@ int brc_create(const brc_config* cfg, void** out) {
     e->bw = e->wide ? (uint32_t)e->npad / 64 : 1u;
     e->nkw_t = e->npad / 8 < 1 ? 1 : e->npad / 8;
     e->NK = (uint32_t)e->npad * c.variants * c.key_window;
-    e->rows = e->wide ? e->NK : e->NK + 1;       // narrow kernel: + the trash row (brc_step.h)
+    // narrow kernel: + the trash row (brc_step.h); connection peers: 3 words per cell
+    e->rows = e->wide ? e->NK : (e->NK + 1) * (c.peer_mode == BRC_PEER_CONNECTION ? 3u : 1u);
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
@@ -511,7 +513,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
-    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, (int)c.mode, blocks, e->lds_bytes, e->stream,
+    const int kmode = c.peer_mode == BRC_PEER_CONNECTION ? KMODE_CONN : (int)c.mode;
+    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
                      e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }

@@ -24,6 +24,7 @@ constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before t
 constexpr uint32_t GEN_MASK_W = 0x7FF;      // wide kernel (n > 64): 11-bit cell generation
 constexpr uint32_t GEN_FULL_CLEAR_W = 1500;
 constexpr int CHUNK_W = 4;                  // wide kernel: keys whose ballots are exchanged per barrier
+constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
 #ifndef BRC_CHUNK
 #define BRC_CHUNK 4
 #endif

@@ -181,6 +181,55 @@ __device__ __forceinline__ void brb_cell_update_beb(uint32_t& fl, bool s_arr, bo
     echo_send = ready_send = false;
 }
 
+// core/brbroadcast.py:60-119 with CONNECTION-identity peers (:69, the reference's local-test mode;
+// SURVEY F1): every message is a new peer address, so the closed form of brb_cell_update holds
+// with ea / ra counting MESSAGES, and the :118-119 amplification re-fires once per qualifying
+// READY -- nothing suppresses the duplicates.  n_ready = READY broadcasts of the cell this step
+// (the :98 one, or the re-fires); F_RS is left to the caller (it marks "has broadcast READY").
+__device__ __forceinline__ void brb_cell_update_conn(uint32_t& fl, uint32_t& ec, uint32_t& rc, bool s_arr,
+                                                     uint32_t ea, uint32_t ra, uint32_t T_echo, uint32_t T_amp,
+                                                     uint32_t T_del, bool& echo_send, uint32_t& n_ready,
+                                                     bool& deliver) {
+    const bool open = !(fl & F_DEL);                                        // :74
+    echo_send = open && s_arr && !(fl & F_EEX);                             // :76-82
+    fl |= echo_send ? (F_EEX | F_ES) : 0u;
+    const bool e_on = open && ea != 0;
+    const uint32_t checked = (fl & F_EEX) ? ea : ea - 1u;                   // :87-89
+    fl |= e_on ? F_EEX : 0u;
+    ec += e_on ? ea : 0u;
+    const bool r1 = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX); // :95-98
+    fl |= r1 ? F_REX : 0u;
+    const bool r_on = open && ra != 0;
+    const bool rex = (fl & F_REX) != 0;
+    const uint32_t lo = rex ? rc + 1u : 2u, hi = rex ? rc + ra : ra;       // :103-108
+    fl |= r_on ? F_REX : 0u;
+    rc += r_on ? ra : 0u;
+    const bool any = r_on && hi >= lo;
+    const uint32_t alo = max(lo, T_amp), ahi = min(hi, T_del - 1u);
+    const uint32_t fires = (any && !(fl & F_EEX) && alo <= ahi) ? ahi - alo + 1u : 0u;   // :118-119, each
+    deliver = any && hi >= T_del;                                           // :111-115
+    fl |= deliver ? F_DEL : 0u;
+    n_ready = (r1 ? 1u : 0u) + fires;
+}
+
+// CONNECTION peers: a lane's send counts of one type over the last 8 steps, one byte per step
+// (slot = step mod 8); `tl` = the last step with a send (NEVER: none).  Valid because a send
+// reaches its receiver within D <= 8 steps and a cell is read before it is written in a step.
+__device__ __forceinline__ uint32_t ring_count(uint64_t ring, uint32_t tl, uint32_t s) {
+    return (tl != NEVER && s <= tl && tl - s < 8u) ? (uint32_t)(ring >> (8u * (s & 7u))) & 0xFFu : 0u;
+}
+__device__ __forceinline__ uint64_t ring_put(uint64_t ring, uint32_t tl, uint32_t t, uint32_t c) {
+    if (tl == NEVER || t - tl >= 8u) {
+        ring = 0;
+    } else if (t != tl) {                        // clear the slots of steps tl+1 .. t
+        const uint32_t m = t - tl, r = 8u * ((tl + 1u) & 7u);
+        const uint64_t mask = (1ull << (8u * m)) - 1u;
+        ring &= ~(r ? ((mask << r) | (mask >> (64u - r))) : mask);
+    }
+    const uint32_t sh = 8u * (t & 7u);
+    return (ring & ~(0xFFull << sh)) | ((uint64_t)min(c, 255u) << sh);
+}
+
 #ifndef BRC_MIN_WAVES
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
@@ -191,7 +240,8 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
     // pinning ~60 of them in SGPRs across the hot loop.  Hot fields are copied to locals below.
     const Params& P = *pp;
-    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
+    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
+    constexpr uint32_t CW = CONN ? 3 : 1;        // u64 words per cell (CONN: + ECHO and READY send rings)
     using T = typename MaskOf<NPAD>::type;
     constexpr int IPW = 64 / NPAD;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -309,7 +359,8 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
-    const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64 + lane;   // cell (k, lane) at [k * 64]
+    // cell (k, lane) at [k * CW * 64] (+ 64, + 128: CONN send rings)
+    const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
@@ -524,15 +575,32 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                         badinj = true;
                     } else {
                         const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
-                        uint64_t wv = mycells[(size_t)k * 64];
-                        if (((wv >> 19) & GEN_MASK) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 19);
+                        uint64_t wv = mycells[(size_t)k * (CW * 64)];
+                        const bool stale = ((wv >> 19) & GEN_MASK) != gen;
+                        if (stale) wv = TIMES_NEVER | ((uint64_t)gen << 19);
                         const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
-                        if (!(wv & bit)) {
+                        const int sh = (r.type == BRC_ECHO) ? 32 : 48;
+                        if constexpr (CONN) {
+                            // every injected broadcast travels: one more send of this type at step t
+                            const size_t ri = (size_t)k * (CW * 64) + ((r.type == BRC_ECHO) ? 64 : 128);
+                            const uint32_t tl = (uint32_t)(wv >> sh) & 0xFFFF;
+                            const uint64_t ring = mycells[ri];
+                            const uint32_t c = ring_count(ring, tl, t) + 1u;
+                            if (c > 31u) {
+                                badinj = true;                      // beyond the 5 count planes
+                            } else {
+                                sent = true;
+                                mycells[ri] = ring_put(ring, tl, t, c);
+                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
+                                wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                                mycells[(size_t)k * (CW * 64)] = wv;
+                                st_msgs += n;
+                            }
+                        } else if (!(wv & bit)) {
                             sent = true;
                             wv |= bit;
-                            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            mycells[(size_t)k * 64] = wv;
+                            mycells[(size_t)k * (CW * 64)] = wv;
                             st_msgs += n;
                             log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
                         }
@@ -597,7 +665,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {     // p < nkeys + CHUNK: padded list
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
-                ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * 64];
+                ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * (CW * 64)];
             });
         };
         auto process = [&](const uint32_t k, const uint64_t wd) {
@@ -612,7 +680,25 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
             const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
             uint32_t ea = 0, ra = 0;
-            {
+            uint64_t ringE = 0, ringR = 0;                       // CONN: this lane's send counts
+            if constexpr (CONN) {
+                ringE = mycells[(size_t)k * (CW * 64) + 64];
+                ringR = mycells[(size_t)k * (CW * 64) + 128];
+                uint32_t j = 0;
+                for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
+                    const uint32_t dly = (uint32_t)__ffs(ds);
+                    const uint32_t ce = ring_count(ringE, tE, t - dly), cr = ring_count(ringR, tR, t - dly);
+                    if (__ballot((ce | cr) != 0)) {               // arrivals = sum over senders of counts:
+                        const T Lj = s_L[j * 64 + lane];         // one ballot per count bit
+#pragma unroll
+                        for (int b = 0; b < 5; ++b) {
+                            const uint64_t be = __ballot((ce >> b) & 1u), br = __ballot((cr >> b) & 1u);
+                            ea += popc((T)(be >> segbase) & Lj) << b;
+                            ra += popc((T)(br >> segbase) & Lj) << b;
+                        }
+                    }
+                }
+            } else {
                 uint32_t j = 0;
                 for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {   // only delays some link has
                     const uint32_t dly = (uint32_t)__ffs(ds);
@@ -639,25 +725,37 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             st_loads += (kl && real_run) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
             bool es, rs, dl;
-            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
+            uint32_t n_ready = 0;                                // CONN: READY broadcasts this step
+            bool first_ready = false;
+            if constexpr (CONN) {
+                brb_cell_update_conn(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, n_ready, dl);
+                rs = n_ready != 0;
+                first_ready = rs && !(fl & F_RS);
+                fl |= rs ? F_RS : 0u;
+                ec = min(ec, 127u); rc = min(rc, 127u);
+                if (es) ringE = ring_put(ringE, tE, t, 1u);
+                if (rs) ringR = ring_put(ringR, tR, t, n_ready);
+                mycells[(size_t)k * (CW * 64) + 64] = ringE;
+                mycells[(size_t)k * (CW * 64) + 128] = ringR;
+            } else if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
             else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {   // whole-wave store (lanes without arrivals write their word back unchanged)
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
                                     ((uint64_t)gen << 19) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
-                mycells[(size_t)k * 64] = has ? nw : wd;
+                mycells[(size_t)k * (CW * 64)] = has ? nw : wd;
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;
-            st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
+            st_msgs += ((es ? 1u : 0u) + (CONN ? n_ready : (rs ? 1u : 0u))) * n;
             st_del += dl ? 1u : 0u;
             if (__ballot(dl))
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
             if (EV) {
                 const uint32_t kp = k / Q, s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
-                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends: ring marks at t + every delay some sending lane has; t_quiet of the key
@@ -838,6 +936,12 @@ int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 
 template <int NPAD>
 int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    if (mode == KMODE_CONN && dm > 8) return BRC_E_INVALID;
+    // connection-identity peers: reference protocol, D <= 8 (brc_create)
+    if (mode == KMODE_CONN && dm == 4) return events ? launch_one<NPAD, 4, true, KMODE_CONN>(blocks, lds, s, P)
+                                                     : launch_one<NPAD, 4, false, KMODE_CONN>(blocks, lds, s, P);
+    if (mode == KMODE_CONN && dm == 8) return events ? launch_one<NPAD, 8, true, KMODE_CONN>(blocks, lds, s, P)
+                                                     : launch_one<NPAD, 8, false, KMODE_CONN>(blocks, lds, s, P);
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
         if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \

@@ -27,14 +27,14 @@ class Engine:
     def __init__(self, n, f, instances, protocol="consensus", seed=0, delay_model=L.DELAY_CONST,
                  delay_max=1, delay_const=1, round_cap=1, step_cap=4000, key_window=4, variants=1,
                  proposals=L.PROPOSALS_NONE, byz_pattern=L.BYZ_NONE, byzantine=(), event_capacity=0,
-                 instance_offset=0, device=0, mode=L.MODE_REFERENCE, coin_seed=0):
+                 instance_offset=0, device=0, mode=L.MODE_REFERENCE, coin_seed=0, peer_mode=L.PEER_SENDER):
         self._lib = L.load()
         self._h = ctypes.c_void_p()
         mask = 0
         for b in byzantine:
             mask |= 1 << int(b)
         proto = {"brb": L.PROTO_BRB, "consensus": L.PROTO_CONSENSUS}.get(protocol, protocol)
-        self.cfg = L.Config(n=n, f=f, protocol=proto, peer_mode=L.PEER_SENDER, instances=instances,
+        self.cfg = L.Config(n=n, f=f, protocol=proto, peer_mode=peer_mode, instances=instances,
                             instance_offset=instance_offset, seed=seed, delay_model=delay_model,
                             delay_max=delay_max, delay_const=delay_const, round_cap=round_cap,
                             step_cap=step_cap, key_window=key_window, variants=variants,

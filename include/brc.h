@@ -53,7 +53,12 @@ enum { BRC_PROTO_BRB = 0, BRC_PROTO_CONSENSUS = 1 };
  * cannot be constructed): a SEND delivers at its arrival, no ECHO/READY; with BRC_PROTO_CONSENSUS
  * the reference's consensus runs on top of it (its consensus_instance.deliver, :42). */
 enum { BRC_MODE_REFERENCE = 0, BRC_MODE_SPEC = 1, BRC_MODE_BEB = 2 };
-enum { BRC_PEER_SENDER = 0 };
+/* Peer identity of core/brbroadcast.py:69-71.  SENDER (:71): sets hold sender ids and the
+ * network drops a message identical to one already sent on the link.  CONNECTION (:69, the
+ * reference's local-test mode): every message is its own connection -- a new peer -- so sets
+ * count messages, nothing is dropped, and the :119 amplification re-fires on every qualifying READY.
+ * CONNECTION needs BRC_MODE_REFERENCE, n <= 64 and delay_max <= 8. */
+enum { BRC_PEER_SENDER = 0, BRC_PEER_CONNECTION = 1 };
 enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DELAY_GEOMETRIC = 3 };
 enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };
 enum { BRC_BYZ_NONE = 0, BRC_BYZ_EQUIVOCATE = 1 };
@@ -66,7 +71,7 @@ typedef struct {
     uint32_t n;               /* replicas per instance, self included (1..256) */
     uint32_t f;               /* fault bound: thresholds (n+f)/2, f+1, 2f+1, n-f+1 */
     uint32_t protocol;        /* BRC_PROTO_* */
-    uint32_t peer_mode;       /* BRC_PEER_SENDER (core/brbroadcast.py:71 identity) */
+    uint32_t peer_mode;       /* BRC_PEER_SENDER / BRC_PEER_CONNECTION (core/brbroadcast.py:69-71) */
     uint64_t instances;       /* instances owned by this engine */
     uint64_t instance_offset; /* global id of instance 0 (Philox counter; multi-GPU shard) */
     uint64_t seed;            /* schedule seed (delays, proposals, slow set) */

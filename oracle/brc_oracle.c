@@ -86,7 +86,8 @@ static inline uint32_t bcount(const bits_t* b) {
 typedef struct {
     uint8_t eex, rex, del;   /* echo_sent_list / ready_sent_list entry exists, delivered */
     uint8_t es, rs;          /* SPEC: ECHO sent, READY sent */
-    bits_t e, r;             /* the two sets (core/brbroadcast.py:38-41) */
+    bits_t e, r;             /* the two sets (core/brbroadcast.py:38-41), sender-identity peers */
+    uint32_t ne, nr;         /* their sizes under connection-identity peers (one peer per message) */
 } cell_t;
 
 typedef struct {
@@ -190,11 +191,12 @@ static int is_honest(const sim_t* S, uint32_t i) {
     return !((S->sp->byz[i >> 6] >> (i & 63)) & 1ull);
 }
 
-/* One link message; duplicate-suppressing network (oracle/schedule.py docstring). */
+/* One link message.  Sender-identity peers: a duplicate-suppressing network (oracle/schedule.py
+ * docstring).  Connection-identity peers: every message travels (each is its own connection). */
 static void net_send(sim_t* S, uint32_t src, uint32_t dst, uint32_t type, int key) {
     key_t_* k = &S->keys[key];
     bits_t* sent = &k->sent[(type - 1) * S->n + src];
-    if (btest(sent, dst)) return;
+    if (S->sp->peer_mode != OR_PEER_CONNECTION && btest(sent, dst)) return;
     int first = !(sent->w[0] | sent->w[1] | sent->w[2] | sent->w[3]);
     bset(sent, dst);
     S->res->msgs_sent++;
@@ -375,8 +377,15 @@ static void beb_on_message(sim_t* S, const msg_t* m) {
     if (S->sp->mode == OR_MODE_BEB_CONSENSUS) cons_deliver(S, m->dst, (int)m->key);
 }
 
-/* core/brbroadcast.py:60-119, one accept-loop iteration at node `dst`; the peer address is
- * the sender id (sender-identity mode, :71). */
+/* set.add(peer_address) then len(set) (core/brbroadcast.py:69-71): a sender id, or a new
+ * connection per message */
+static uint32_t peer_add(const sim_t* S, bits_t* set, uint32_t* cnt, uint32_t src) {
+    if (S->sp->peer_mode == OR_PEER_CONNECTION) return ++*cnt;
+    bset(set, src);
+    return bcount(set);
+}
+
+/* core/brbroadcast.py:60-119, one accept-loop iteration at node `dst`. */
 static void brb_on_message(sim_t* S, const msg_t* m) {
     key_t_* k = &S->keys[m->key];
     cell_t* c = &k->cells[m->dst];
@@ -385,30 +394,32 @@ static void brb_on_message(sim_t* S, const msg_t* m) {
     if (c->del) return;                                       /* :74 */
     if (m->type == OR_SEND) {
         if (!c->eex) {                                        /* :76 */
-            c->eex = 1; memset(&c->e, 0, sizeof(bits_t));     /* :79 */
+            c->eex = 1; memset(&c->e, 0, sizeof(bits_t)); c->ne = 0;   /* :79 */
             net_broadcast(S, m->dst, OR_ECHO, (int)m->key);   /* :82 */
         }
     } else if (m->type == OR_ECHO) {
         if (!c->eex) {                                        /* :87-89: no threshold check */
-            c->eex = 1; memset(&c->e, 0, sizeof(bits_t)); bset(&c->e, m->src);
+            c->eex = 1; memset(&c->e, 0, sizeof(bits_t)); c->ne = 0;
+            peer_add(S, &c->e, &c->ne, m->src);
         } else {
-            bset(&c->e, m->src);                              /* :92 */
-            if (2u * bcount(&c->e) > n + f && !c->rex) {      /* :95 */
-                c->rex = 1; memset(&c->r, 0, sizeof(bits_t)); /* :96 */
+            const uint32_t ne = peer_add(S, &c->e, &c->ne, m->src);   /* :92 */
+            if (2u * ne > n + f && !c->rex) {                 /* :95 */
+                c->rex = 1; memset(&c->r, 0, sizeof(bits_t)); c->nr = 0;   /* :96 */
                 net_broadcast(S, m->dst, OR_READY, (int)m->key);  /* :98 */
             }
         }
     } else if (m->type == OR_READY) {
         if (!c->rex) {                                        /* :103-105: no check */
-            c->rex = 1; memset(&c->r, 0, sizeof(bits_t)); bset(&c->r, m->src);
+            c->rex = 1; memset(&c->r, 0, sizeof(bits_t)); c->nr = 0;
+            peer_add(S, &c->r, &c->nr, m->src);
         } else {
-            bset(&c->r, m->src);                              /* :108 */
-            if (bcount(&c->r) > 2 * f) {                      /* :111 */
+            const uint32_t nr = peer_add(S, &c->r, &c->nr, m->src);   /* :108 */
+            if (nr > 2 * f) {                                 /* :111 */
                 c->del = 1;                                   /* :112 */
                 uint32_t ev[4] = {S->t, m->dst, k->kp, k->s};
                 push_event(S->res->deliver, S->res->deliver_cap, &S->res->n_deliver, 4, ev);
                 if (S->sp->mode == OR_MODE_CONSENSUS) cons_deliver(S, m->dst, (int)m->key);  /* :115 */
-            } else if (!c->eex && bcount(&c->r) > f) {        /* :118 */
+            } else if (!c->eex && nr > f) {                   /* :118 */
                 net_broadcast(S, m->dst, OR_READY, (int)m->key);  /* :119 (re-fires) */
             }
         }

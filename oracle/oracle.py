@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
 ACT = {"propose": 1, "brb_send": 2, "byz_key": 3, "byz": 4}
 STATUS = {1: "done", 2: "quiescent", 3: "stepcap", 4: "overflow"}
+PEER_MODES = {"sender": 0, "connection": 1}
 MODES = {"brb": 0, "consensus": 1, "spec": 2, "spec_brb": 3, "beb": 4, "beb_consensus": 5}
 
 
@@ -28,7 +29,7 @@ class _Spec(ctypes.Structure):
                 ("dmax", ctypes.c_uint32), ("dconst", ctypes.c_uint32), ("round_cap", ctypes.c_uint32),
                 ("g", ctypes.c_uint64), ("step_cap", ctypes.c_uint32), ("n_actions", ctypes.c_uint32),
                 ("byz", ctypes.c_uint64 * 4), ("actions", ctypes.POINTER(_Action)),
-                ("coin_seed", ctypes.c_uint64), ("window", ctypes.c_uint32), ("pad", ctypes.c_uint32)]
+                ("coin_seed", ctypes.c_uint64), ("window", ctypes.c_uint32), ("peer_mode", ctypes.c_uint32)]
 
 
 class _Result(ctypes.Structure):
@@ -97,7 +98,8 @@ def run(spec):
                nv=spec.get("nv", 1), seed=spec["seed"], delay_model=spec["delay_model"],
                dmax=spec["dmax"], dconst=spec.get("dconst", 1), round_cap=spec.get("round_cap", 0),
                g=spec["g"], step_cap=spec.get("step_cap", 10000), n_actions=len(acts),
-               byz=_mask4(byz), actions=arr, coin_seed=spec.get("coin_seed", 0), window=spec.get("window", 0))
+               byz=_mask4(byz), actions=arr, coin_seed=spec.get("coin_seed", 0), window=spec.get("window", 0),
+               peer_mode=PEER_MODES[spec.get("peer_mode", "sender")])
     cap = 4096
     while True:
         bufs = [(ctypes.c_uint32 * (cap * w))() for w in (4, 4, 5)]

@@ -23,7 +23,7 @@ def sort_result(res):
 def _cfg_key(sp):
     return (sp["n"], sp["f"], sp["mode"], sp.get("nv", 1), sp["seed"], sp["delay_model"], sp["dmax"],
             sp.get("dconst", 1), sp.get("round_cap", 0), sp.get("step_cap", 10000),
-            tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"))
+            tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"), sp.get("peer_mode", "sender"))
 
 
 def _injections(sp, local):
@@ -72,6 +72,7 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
                  round_cap=sp0.get("round_cap", 0), step_cap=sp0.get("step_cap", 10000), key_window=key_window,
                  variants=sp0.get("nv", 1), byzantine=sp0.get("byzantine", ()), event_capacity=event_capacity,
                  instance_offset=sp0["g"], device=device, mode=mode,
+                 peer_mode=L.PEER_CONNECTION if sp0.get("peer_mode") == "connection" else L.PEER_SENDER,
                  coin_seed=sp0.get("coin_seed", 0))
     try:
         inj = []

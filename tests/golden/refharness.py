@@ -12,9 +12,12 @@ How the reference is driven
   ``sendall`` to the simulated network; the sender is found by walking the caller frames
   up to ``Broadcast.broadcast`` (its ``self.host``).  The server socket
   (``core/brbroadcast.py:55-62``) blocks in ``accept()`` until the scheduler hands it ONE
-  message, and returns ``(sender_name, 0)`` as the peer address, so the reference's
-  ``peer_address`` (``core/brbroadcast.py:69``) is the stable sender identity
-  ("sender-identity" peer mode).
+  message, and returns ``(sender_name, port)`` as the peer address.  Sender-identity peers
+  (``spec["peer_mode"] == "sender"``, the default): ``port`` is 0, so the reference's
+  ``peer_address`` (``core/brbroadcast.py:69``) is the stable sender identity and the network
+  drops duplicates.  Connection-identity peers (``"connection"``, the reference's local-test
+  behaviour): ``port`` is a fresh number per message, as an ephemeral TCP port is, and nothing
+  is dropped.
 * ``threading`` stays real: every node runs its own listener thread
   (``core/brbroadcast.py:121-128``).  The scheduler hands over one message, then waits until
   that node is back in ``accept()`` -- so exactly one message is in processing at any time
@@ -136,14 +139,14 @@ class _Server:
             self.idle = False
         if item == "shutdown":
             raise SystemExit()   # ends the listener thread silently
-        data, sender_name = item
-        return _Conn(data), (sender_name, 0)
+        data, sender_name, port = item
+        return _Conn(data), (sender_name, port)
 
-    def hand(self, data, sender_name, timeout=30.0):
+    def hand(self, data, sender_name, port=0, timeout=30.0):
         with self.cv:
             if not self.idle:
                 raise HarnessError("node %r not idle" % (self.addr,))
-            self.item = (data, sender_name)
+            self.item = (data, sender_name, port)
             self.idle = False
             self.cv.notify_all()
             ok = self.cv.wait_for(lambda: self.idle or self.failed, timeout)
@@ -182,6 +185,8 @@ class Run:
         self.nv = spec.get("nv", 1)
         self.g = spec["g"]
         self.mode = spec["mode"]
+        self.connection = spec.get("peer_mode", "sender") == "connection"
+        self.ports = 0
         self.byz = set(spec.get("byzantine", []))
         self.honest = [i for i in range(self.n) if i not in self.byz]
         self.values = spec["values"]
@@ -236,9 +241,10 @@ class Run:
         payload, mtype = env["message"], env["type"]
         kp, s = self.key_for(payload)
         ident = (src, dst, mtype, payload)
-        if ident in self.sent:          # duplicate-suppressing network
-            return
-        self.sent.add(ident)
+        if not self.connection:
+            if ident in self.sent:      # duplicate-suppressing network (sender-identity peers)
+                return
+            self.sent.add(ident)
         self.msgs_sent += 1
         self.wire.append([self.t, src, dst, data.decode("utf-8")])
         fs = (src, mtype, payload)
@@ -370,7 +376,8 @@ class Run:
                     for order, dst, data, src in msgs:
                         if dst in self.servers:
                             self.arrivals_processed += 1
-                            self.servers[dst].hand(data, "n%d" % src)
+                            self.ports += 1
+                            self.servers[dst].hand(data, "n%d" % src, self.ports if self.connection else 0)
                     for a in actions.pop(nt, []):
                         self.act(a)
                     if self.mode == "consensus" and rcap > 0 and all(

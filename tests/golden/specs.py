@@ -24,18 +24,19 @@ def _sched(n, f, seed, model, dmax, dconst=1):
     return Schedule(n, f, seed, model, dmax, dconst)
 
 
-def brb_spec(n, f, seed, model, dmax, g, sends, dconst=1, byzantine=(), extra=(), step_cap=10000):
+def brb_spec(n, f, seed, model, dmax, g, sends, dconst=1, byzantine=(), extra=(), step_cap=10000,
+             peer_mode="sender"):
     """sends: list of (t, origin, seq)."""
     acts = [dict(t=t, kind="brb_send", node=o, kp=o, s=q, payload="TEST %d.%d" % (o + 1, q))
             for (t, o, q) in sends]
     acts += list(extra)
     return dict(n=n, f=f, mode="brb", nv=1, seed=seed, delay_model=model, dmax=dmax, dconst=dconst,
                 g=g, byzantine=list(byzantine), values=VALUES, round_cap=0, step_cap=step_cap,
-                actions=acts)
+                actions=acts, peer_mode=peer_mode)
 
 
 def cons_spec(n, f, seed, model, dmax, g, round_cap=2, proposals=None, byzantine=(), nv=1,
-              starts=None, dconst=1, extra=(), step_cap=4000):
+              starts=None, dconst=1, extra=(), step_cap=4000, peer_mode="sender"):
     """proposals: None -> Philox Bernoulli(1/2) value ids; or a list of value ids.
     starts: None -> every honest replica proposes at t=0; or a list of start times."""
     sch = _sched(n, f, seed, model, dmax, dconst)
@@ -48,7 +49,7 @@ def cons_spec(n, f, seed, model, dmax, g, round_cap=2, proposals=None, byzantine
     acts += list(extra)
     return dict(n=n, f=f, mode="consensus", nv=nv, seed=seed, delay_model=model, dmax=dmax,
                 dconst=dconst, g=g, byzantine=list(byzantine), values=VALUES, round_cap=round_cap,
-                step_cap=step_cap, actions=acts)
+                step_cap=step_cap, actions=acts, peer_mode=peer_mode)
 
 
 def spec_cons_spec(n, f, seed, model, dmax, g, round_cap=1, window=4, coin_seed=0xC01D, **kw):
@@ -230,6 +231,18 @@ def scenario_groups():
     G["brb_slowset_n256"] = [brb_spec(256, 85, 0x5EED0005, 2, 8, g, [(0, 130, 0)]) for g in range(1)]
     G["cons_uniform_n70"] = [cons_spec(70, 23, 0x5EED0005, 1, 4, g, round_cap=1) for g in range(1)]
     G["cons_slowset_n70"] = [cons_spec(70, 23, 0x5EED0005, 2, 8, g, round_cap=1) for g in range(1)]
+    # connection-identity peers (core/brbroadcast.py:69, the reference's local-test mode)
+    G["conn_kat"] = [clone(sp, peer_mode="connection", name=sp["name"] + "-conn")
+                     for sp in kat_specs().values()]
+    G["conn_brb_slowset_n7"] = [brb_spec(7, 2, 0xC0AA, 2, 5, g, [(0, i, 0) for i in range(7)], peer_mode="connection")
+                                for g in range(4)]
+    G["conn_cons_slowset_n7"] = [cons_spec(7, 2, 0xC0AB, 2, 4, g, round_cap=2, peer_mode="connection")
+                                 for g in range(6)]
+    G["conn_cons_uniform_n6"] = [cons_spec(6, 1, 0xC0AC, 1, 3, g, round_cap=2, peer_mode="connection")
+                                 for g in range(8)]
+    G["conn_cons_byz_n16"] = [cons_spec(16, 5, 0x5EED0003, m, d, g, round_cap=1, byzantine=list(range(11, 16)), nv=2,
+                                        extra=equivocation_actions(16, list(range(11, 16))), peer_mode="connection")
+                              for (m, d) in ((1, 4), (2, 4)) for g in range(2)]
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))

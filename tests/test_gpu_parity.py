@@ -93,3 +93,50 @@ def test_staggered_starts_vs_oracle(runner):
         sp["name"] = "stag/%d" % g
         specs.append(sp)
     _compare_with_oracle(runner, specs)
+
+
+# ---- connection-identity peers (core/brbroadcast.py:69) ----
+@pytest.mark.parametrize("n,f,model,dmax", [(4, 1, 1, 4), (7, 2, 3, 6), (16, 5, 2, 8), (33, 10, 1, 3), (64, 21, 2, 8)])
+def test_connection_brb_floods_vs_oracle(runner, n, f, model, dmax):
+    """Honest broadcasts plus Byzantine nodes that re-send ECHO / READY of honest keys at several
+    steps: every copy is a new peer, so the counts (and K4 re-fires) differ from sender mode."""
+    rng = random.Random(n * 31 + dmax)
+    allm = (1 << n) - 1
+    specs = []
+    for g in range(24 if n <= 16 else 6):
+        byz = rng.sample(range(n), f)
+        honest = [o for o in range(n) if o not in byz]
+        sends = [(rng.randint(0, 3), o, 0) for o in rng.sample(honest, min(len(honest), 4))]
+        extra = []
+        for (t0, o, q) in sends:
+            for b in rng.sample(byz, min(len(byz), 3)):
+                for _ in range(rng.randint(1, 3)):
+                    extra.append(dict(t=t0 + rng.randint(0, 6), kind="byz", src=b, type=rng.choice([2, 3]),
+                                      kp=o, s=q, dst=allm))
+        sp = S.brb_spec(n, f, 0xC0 + n, model, dmax, 900 + g, sends, byzantine=byz, extra=extra,
+                        peer_mode="connection")
+        sp["name"] = "connbrb%d/%d" % (n, g)
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+@pytest.mark.parametrize("n,f,model,dmax,rcap", [(4, 1, 1, 4, 3), (7, 2, 2, 4, 2), (10, 3, 3, 5, 2),
+                                                  (16, 5, 2, 8, 2), (64, 21, 2, 8, 1)])
+def test_connection_consensus_vs_oracle(runner, n, f, model, dmax, rcap):
+    specs = []
+    for g in range(24 if n <= 16 else 4):
+        sp = S.cons_spec(n, f, 0xC0C0 + n, model, dmax, 40 + g, round_cap=rcap, peer_mode="connection")
+        sp["name"] = "conncons%d/%d" % (n, g)
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+def test_connection_equivocation_vs_oracle(runner):
+    byz = list(range(11, 16))
+    specs = []
+    for g in range(16):
+        sp = S.cons_spec(16, 5, 0x5EED0003, 1, 4, 3100 + g, round_cap=1, byzantine=byz, nv=2,
+                         extra=S.equivocation_actions(16, byz), peer_mode="connection")
+        sp["name"] = "conncfg3/%d" % g
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)

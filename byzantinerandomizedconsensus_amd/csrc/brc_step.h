@@ -146,7 +146,7 @@ __device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint
     rc += r_on ? ra : 0u;
     const bool any = r_on && hi >= lo;
     const uint32_t alo = max(lo, T_amp), ahi = min(hi, T_del - 1u);
-    const bool r2 = any && !(fl & F_EEX) && alo <= ahi && !(fl & F_RS);    // :118-119
+    const bool r2 = any & !(fl & F_EEX) & (alo <= ahi) & !(fl & F_RS);      // :118-119
     fl |= r2 ? F_RS : 0u;
     deliver = any && hi >= T_del;                                           // :111-115
     fl |= deliver ? F_DEL : 0u;
@@ -350,6 +350,11 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     }
     const uint32_t maxout = hibit(outset);
     const uint32_t dset = uni32(wave_or(outset));    // every delay some link of this wave has
+    // dlist: the delays present, minus one, 4 bits each in ascending order; ndl of them
+    uint64_t dlist = 0;
+    uint32_t ndl = 0;
+    for (uint32_t ds = dset; ds; ds &= ds - 1) dlist |= (uint64_t)(__ffs(ds) - 1) << (4 * ndl++);
+    dlist = uni64(dlist); ndl = uni32(ndl);
     // compact delay masks: the j-th delay present in the wave -> s_L[j]; every nonzero L[i] of an
     // honest receiver is in dset (its sender's outset has bit i)
     {
@@ -699,16 +704,18 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                     }
                 }
             } else {
-                uint32_t j = 0;
-                for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {   // only delays some link has
-                    const uint32_t dly = (uint32_t)__ffs(ds);
-                    const uint64_t be = __ballot(dE == dly), br = __ballot(dR == dly);
-                    if (be | br) {
+                // the j-th delay present in the wave, precomputed (dlist), unrolled, and no test for
+                // empty ballots: a branch per delay cost more than the popcounts it skipped (r1 A/B)
+                Unrolled<DM>::run([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if ((uint32_t)j < ndl) {
+                        const uint32_t dly = (dlist >> (4 * j)) & 15u;
+                        const uint64_t be = __ballot(dE == dly + 1u), br = __ballot(dR == dly + 1u);
                         const T Lj = s_L[j * 64 + lane];
                         ea += popc((T)(be >> segbase) & Lj);
                         ra += popc((T)(br >> segbase) & Lj);
                     }
-                }
+                });
             }
             // SEND from the key's origin: arrives at t_send + delay(origin -> d)
             bool s_arr = false;

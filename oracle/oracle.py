@@ -79,8 +79,9 @@ def philox(ctr, key):
     return tuple(out)
 
 
-def run(spec):
-    """Run one instance of ``spec`` (harness format) and return the harness result format."""
+def run(spec, light=False):
+    """Run one instance of ``spec`` (harness format) and return the harness result format.
+    ``light``: status and counters only (no event lists; one C call, no Python conversion)."""
     acts = sorted(spec.get("actions", []), key=lambda a: a["t"])
     arr = (_Action * max(1, len(acts)))()
     for i, a in enumerate(acts):
@@ -100,7 +101,7 @@ def run(spec):
                g=spec["g"], step_cap=spec.get("step_cap", 10000), n_actions=len(acts),
                byz=_mask4(byz), actions=arr, coin_seed=spec.get("coin_seed", 0), window=spec.get("window", 0),
                peer_mode=PEER_MODES[spec.get("peer_mode", "sender")])
-    cap = 4096
+    cap = 0 if light else 4096
     while True:
         bufs = [(ctypes.c_uint32 * (cap * w))() for w in (4, 4, 5)]
         res = _Result(deliver=bufs[0], deliver_cap=cap, decide=bufs[1], decide_cap=cap,
@@ -108,9 +109,14 @@ def run(spec):
         rc = lib().oracle_run(ctypes.byref(sp), ctypes.byref(res))
         if rc != 0:
             raise RuntimeError("oracle_run failed: %d" % rc)
-        if max(res.n_deliver, res.n_decide, res.n_send) <= cap:
+        if light or max(res.n_deliver, res.n_decide, res.n_send) <= cap:
             break
         cap = 2 * max(res.n_deliver, res.n_decide, res.n_send)
+
+    if light:
+        return {"status": STATUS.get(res.status), "t_stop": res.t_stop, "msgs_sent": res.msgs_sent,
+                "arrivals": res.arrivals,
+                "counts": {"deliver": res.n_deliver, "decide": res.n_decide, "send": res.n_send}}
 
     def rows(buf, cnt, w):
         return [list(buf[i * w:(i + 1) * w]) for i in range(cnt)]

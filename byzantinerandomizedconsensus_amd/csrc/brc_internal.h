@@ -68,19 +68,21 @@ __host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) 
     return model == BRC_DELAY_CONST ? 1u : model == BRC_DELAY_SLOWSET ? (dmax > 1 ? 2u : 1u) : dmax;
 }
 
-// u64 words of a wave's consensus LDS area: REFERENCE hm[4][64] T; SPEC seen[Q][64] T + cnt[Q][64] u32
-__host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32_t Q) {
-    return spec ? (Q * 64 * msize + Q * 64 * 4 + 7) / 8 : (4 * 64 * msize + 7) / 8;
+// u64 words of a wave's consensus LDS area: REFERENCE hm[4][64] T; SPEC [seen[Q][64] T +] cnt[Q][64] u32
+__host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32_t Q, uint32_t nv) {
+    // SPEC with one key variant per origin: a replica delivers each (origin, phase) key at most
+    // once, so the origin count needs no host set (seen masks only when nv > 1)
+    return spec ? (Q * 64 * (nv > 1 ? msize : 0u) + Q * 64 * 4 + 7) / 8 : (4 * 64 * msize + 7) / 8;
 }
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u32 (tail padded with the trash row NK)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
-                                                       uint32_t Q) {
+                                                       uint32_t Q, uint32_t nv) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
-    const uint32_t h_words = cons_words(spec, msize, Q);
+    const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 2 * CHUNK + 1) / 2);
 }
@@ -102,8 +104,8 @@ __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32
 
 // Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of
 // n bits; SPEC phase windows seen[Q][lanes] (n bits; narrow kernel only) + cnt[Q][lanes] u32.
-inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32_t msize, uint32_t Q) {
-    return spec ? (uint64_t)Q * lanes * ((wide ? 0 : msize) + 4) : 4ull * lanes * msize;
+inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32_t msize, uint32_t Q, uint32_t nv) {
+    return spec ? (uint64_t)Q * lanes * ((wide || nv == 1 ? 0 : msize) + 4) : 4ull * lanes * msize;
 }
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).

@@ -255,14 +255,16 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK] u32
     // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
     const uint32_t nL = P.nL;
-    const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q);
+    const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
+    const bool seen_on = NV > 1;                 // SPEC: host sets needed only with key variants
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q) / 8);
+    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV) / 8);
     uint64_t* s_act = s_meta + IPW * NK;
     uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
     T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
-    T* s_seen = s_hm;                            // SPEC: s_seen[q*64 + lane]: hosts delivered for phase slot q
-    uint32_t* s_cnt = (uint32_t*)(s_seen + Q * 64); // SPEC: s_cnt[q*64 + lane]: #"0" | #"1" << 16
+    T* s_seen = s_hm;                            // SPEC, NV > 1: s_seen[q*64 + lane]: hosts delivered for phase slot q
+    // SPEC: s_cnt[q*64 + lane] = #origins | #"0" << 10 | #"1" << 20 for phase slot q
+    uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
     uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
     uint32_t* s_klist = s_gen + ((IPW * NK + 1) & ~1u); // this step's active key slots
@@ -374,9 +376,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     if (cons_lane) { c0 = gp(P.cons0)[li]; c1 = gp(P.cons1)[li]; }
     if constexpr (SPEC) {
         const T* gseen = (const T*)P.hmask;
-        const uint32_t* gcnt = (const uint32_t*)((const char*)P.hmask + P.nitems * Q * 64 * sizeof(T));
+        const uint32_t* gcnt = (const uint32_t*)((const char*)P.hmask + (seen_on ? P.nitems * Q * 64 * sizeof(T) : 0));
         for (uint32_t q = 0; q < Q; ++q) {
-            s_seen[q * 64 + lane] = cons_lane ? gp(gseen)[(item * Q + q) * 64 + lane] : (T)0;
+            if (seen_on) s_seen[q * 64 + lane] = cons_lane ? gp(gseen)[(item * Q + q) * 64 + lane] : (T)0;
             s_cnt[q * 64 + lane] = cons_lane ? gp(gcnt)[(item * Q + q) * 64 + lane] : 0u;
         }
     } else {
@@ -467,9 +469,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     auto spec_advance = [&]() {
         while (round > 0) {
             const uint32_t s = 2 * (round - 1) + (phase - 1), q = s % Q;
-            if (popc(s_seen[q * 64 + lane]) < n - P.f) return;
-            const uint32_t cc = s_cnt[q * 64 + lane], n0 = cc & 0xFFFF, n1 = cc >> 16;
-            s_seen[q * 64 + lane] = 0;
+            const uint32_t cc = s_cnt[q * 64 + lane], n0 = (cc >> 10) & 0x3FF, n1 = cc >> 20;
+            if ((seen_on ? popc(s_seen[q * 64 + lane]) : (cc & 0x3FF)) < n - P.f) return;
+            if (seen_on) s_seen[q * 64 + lane] = 0;
             s_cnt[q * 64 + lane] = 0;
             if (phase == 1) {
                 const uint32_t prop = (2 * n0 > n + P.f) ? 1u : (2 * n1 > n + P.f) ? 2u : 0u;
@@ -501,10 +503,11 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         if (s < cur) return;
         if (s >= cur + Q) { ovf = true; return; }
         const uint32_t q = s % Q;
-        if ((s_seen[q * 64 + lane] >> host) & 1) return;
-        s_seen[q * 64 + lane] |= (T)((T)1 << host);
-        if (v == 1) s_cnt[q * 64 + lane] += 1u;
-        else if (v == 2) s_cnt[q * 64 + lane] += 1u << 16;
+        if (seen_on) {
+            if ((s_seen[q * 64 + lane] >> host) & 1) return;
+            s_seen[q * 64 + lane] |= (T)((T)1 << host);
+        }
+        s_cnt[q * 64 + lane] += 1u + (v == 1 ? 1u << 10 : 0u) + (v == 2 ? 1u << 20 : 0u);
         spec_advance();
     };
 
@@ -887,9 +890,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                       ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
         if constexpr (SPEC) {
             T* gseen = (T*)P.hmask;
-            uint32_t* gcnt = (uint32_t*)((char*)P.hmask + P.nitems * Q * 64 * sizeof(T));
+            uint32_t* gcnt = (uint32_t*)((char*)P.hmask + (seen_on ? P.nitems * Q * 64 * sizeof(T) : 0));
             for (uint32_t q = 0; q < Q; ++q) {
-                gp(gseen)[(item * Q + q) * 64 + lane] = s_seen[q * 64 + lane];
+                if (seen_on) gp(gseen)[(item * Q + q) * 64 + lane] = s_seen[q * 64 + lane];
                 gp(gcnt)[(item * Q + q) * 64 + lane] = s_cnt[q * 64 + lane];
             }
         } else {

@@ -77,14 +77,14 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
-// mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u32 (tail padded with the trash row NK)
+// mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u16 (tail padded with the trash row NK)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
-    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 2 * CHUNK + 1) / 2);
+    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 2 * CHUNK + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
-    //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK] u32
+    //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u16
     // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
     const uint32_t nL = P.nL;
     const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
     uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
-    uint32_t* s_klist = s_gen + ((IPW * NK + 1) & ~1u); // this step's active key slots
+    uint16_t* s_klist = (uint16_t*)(s_gen + ((IPW * NK + 1) & ~1u)); // this step's active key slots
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -665,10 +665,10 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             const uint64_t bits = uni64(s_act[row * nkw + w]);
             const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
-            if ((bits >> lane) & 1) s_klist[nkeys + below] = w * 64 + lane;
+            if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)(w * 64 + lane);
             nkeys += (uint32_t)__popcll(bits);
         }
-        if (lane < 2 * CHUNK) s_klist[nkeys + lane] = NK;   // chunk padding -> the trash row
+        if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {     // p < nkeys + CHUNK: padded list
             Unrolled<CHUNK>::run([&](auto ci) {

@@ -113,6 +113,7 @@ struct Engine {
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
     uint32_t rows = 0;                           // cell rows per item
+    uint32_t rs = TS;                            // activity-ring rows (narrow kernel: ring_steps(dm))
     uint64_t cons_bytes = 0;                     // consensus-set buffer (hmask) bytes per item
     uint64_t nitems = 0;
     hipStream_t stream = nullptr;
@@ -200,7 +201,7 @@ static int clear_state(Engine* e, bool full) {
                            (uint64_t)keys);
         HIPCHK(e, hipGetLastError());
     }
-    HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * TS * e->nkw * 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->actany, 0, (size_t)e->nitems * 4, e->stream));
     HIPCHK(e, hipMemsetAsync(e->items, 0, (size_t)e->nitems * sizeof(ItemState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->inst, 0, (size_t)e->cfg.instances * sizeof(InstState), e->stream));
@@ -309,6 +310,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->cfg = c;
     e->npad = pick_npad(c.n);
     e->dm = pick_dm(c.delay_max);
+    e->rs = (c.n > 64) ? (uint32_t)TS : ring_steps(e->dm);
     e->wide = e->npad > 64;
     e->ipw = e->wide ? 1 : 64 / e->npad;
     e->lpi = e->wide ? (uint32_t)e->npad : 64u;
@@ -323,7 +325,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, nL, spec, c.key_window)
-                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window, c.variants) * WPB;
+                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window, c.variants, e->rs) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
@@ -342,7 +344,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, cells * 8}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
-        {(void**)&e->kdst, keys * 8}, {(void**)&e->act, (size_t)e->nitems * TS * e->nkw * 8},
+        {(void**)&e->kdst, keys * 8}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},

@@ -19,6 +19,15 @@ constexpr uint64_t TIMES_NEVER = 0xFFFFFFFF00000000ull;
 constexpr uint32_t F_EEX = 1, F_REX = 2, F_DEL = 4, F_ES = 8, F_RS = 16;
 constexpr uint32_t GEN_MASK = 0x1FFF;
 constexpr uint32_t GEN_RESTRICTED = 0x80000000u;
+constexpr uint32_t GEN16_RESTRICTED = 0x8000u;  // the narrow kernel's 16-bit LDS copy of mgen
+__host__ __device__ inline uint16_t gen16(uint32_t g) {
+    return (uint16_t)((g & GEN_MASK) | ((g & GEN_RESTRICTED) ? GEN16_RESTRICTED : 0u));
+}
+__host__ __device__ inline uint32_t gen32(uint16_t g) {
+    return (g & GEN_MASK) | ((g & GEN16_RESTRICTED) ? GEN_RESTRICTED : 0u);
+}
+// activity-ring rows of the narrow kernel: a power of two above the largest delay (D <= DM)
+__host__ __device__ constexpr uint32_t ring_steps(int dm) { return dm <= 8 ? 16u : 32u; }
 constexpr uint32_t STEP_LIMIT = 60000;
 constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
 constexpr uint32_t GEN_MASK_W = 0x7FF;      // wide kernel (n > 64): 11-bit cell generation
@@ -76,15 +85,15 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 }
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
-// meta[IPW*NK] u64 | act[TS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
-// mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u16 (tail padded with the trash row NK)
+// meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
+// mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16 (tail padded with the trash row NK)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
-                                                       uint32_t Q, uint32_t nv) {
+                                                       uint32_t Q, uint32_t nv, uint32_t rs) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
-    return 8 * (ipw * NK + TS * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 1) / 2 + (NK + 2 * CHUNK + 3) / 4);
+    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 3) / 4 + (NK + 2 * CHUNK + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

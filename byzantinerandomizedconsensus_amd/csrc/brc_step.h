@@ -243,6 +243,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     constexpr uint32_t CW = CONN ? 3 : 1;        // u64 words per cell (CONN: + ECHO and READY send rings)
     using T = typename MaskOf<NPAD>::type;
+    constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
     constexpr int IPW = 64 / NPAD;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
@@ -252,22 +253,22 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
-    //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u32 | klist[NK + 2 CHUNK] u16
+    //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16
     // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
     const uint32_t nL = P.nL;
     const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
     const bool seen_on = NV > 1;                 // SPEC: host sets needed only with key variants
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV) / 8);
+    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV, RS) / 8);
     uint64_t* s_act = s_meta + IPW * NK;
-    uint64_t* s_dbits = s_act + TS * nkw;        // this step's deliveries, per lane
+    uint64_t* s_dbits = s_act + RS * nkw;        // this step's deliveries, per lane
     T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
     T* s_seen = s_hm;                            // SPEC, NV > 1: s_seen[q*64 + lane]: hosts delivered for phase slot q
     // SPEC: s_cnt[q*64 + lane] = #origins | #"0" << 10 | #"1" << 20 for phase slot q
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
-    uint32_t* s_gen = (uint32_t*)(s_dbits + 64 * nkw + h_words + l_words);
-    uint16_t* s_klist = (uint16_t*)(s_gen + ((IPW * NK + 1) & ~1u)); // this step's active key slots
+    uint16_t* s_gen = (uint16_t*)(s_dbits + 64 * nkw + h_words + l_words);   // gen | GEN16_RESTRICTED
+    uint16_t* s_klist = s_gen + ((IPW * NK + 3) & ~3u);                      // this step's active key slots
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -286,9 +287,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
             const bool ok = item * IPW + i / NK < P.instances;
             s_meta[i] = ok ? gp(P.meta)[mb + i] : 0ull;
-            s_gen[i] = ok ? gp(P.mgen)[mb + i] : 0u;
+            s_gen[i] = ok ? gen16(gp(P.mgen)[mb + i]) : (uint16_t)0;
         }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) s_act[i] = gp(P.act)[item * TS * nkw + i];
+        for (uint32_t i = lane; i < RS * nkw; i += 64) s_act[i] = gp(P.act)[item * RS * nkw + i];
         for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
     }
     uint32_t any_rows = uni32(gp(P.actany)[item]);   // ring rows holding any marked key (wave-uniform)
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     auto mark_lane = [&](uint32_t k, uint32_t ds) {
         while (ds) {
             const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
-            const uint32_t row = (t + i + 1) & (TS - 1);
+            const uint32_t row = (t + i + 1) & (RS - 1);
             atomicOr((unsigned long long*)&s_act[row * nkw + (k >> 6)], 1ull << (k & 63));
             lane_rows |= 1u << row;
         }
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         const uint32_t k = (d * NV) * Q + (s % Q);
         const uint64_t m = s_meta[mbase + k];
         if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
-        s_gen[mbase + k] = ((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK;
+        s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
@@ -562,7 +563,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[mbase + k] = m;
                             const bool restricted = is_send && (r.dst & all64) != all64;
-                            s_gen[mbase + k] = gen | (restricted ? GEN_RESTRICTED : 0u);
+                            s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 gp(P.kdst)[inst * NK + k] = r.dst;
@@ -647,14 +648,15 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         const bool running = IPW == 1 || running0;       // one instance per wave: it is running
         const bool hon_run = honest && running, real_run = real && running;
         // next step with possible arrivals (activity ring) or a pending action
-        const uint32_t rot = (t + 1) & (TS - 1);
-        const uint32_t rr = rot ? ((any_rows >> rot) | (any_rows << (TS - rot))) : any_rows;
+        const uint32_t rot = (t + 1) & (RS - 1);
+        const uint32_t rr = (rot ? ((any_rows >> rot) | (any_rows << (RS - rot))) : any_rows) &
+                            (RS == 32 ? ~0u : ((1u << RS) - 1u));
         uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
         if (inj_pos < inj_cnt) next = min(next, gp(P.inj)[inj_off + inj_pos].t);
         if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
         if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
         t = next;
-        const uint32_t row = t & (TS - 1);
+        const uint32_t row = t & (RS - 1);
 
         // ================= BRB: the step's active key slots; one (receiver, key) cell per lane.
         // The ring row becomes a key list (marks made now land on other rows, so it is fixed);
@@ -727,7 +729,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             const bool s_win = kl && dt - 1u < D && (dset & bit) != 0;     // uniform if IPW == 1
             if (IPW == 1 ? s_win : __any(s_win)) {
                 bool hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> m_sender(m)) & 1;
-                if (IPW == 1 ? (gw & GEN_RESTRICTED) != 0 : __any((gw & GEN_RESTRICTED) != 0))
+                if (IPW == 1 ? (gw & GEN16_RESTRICTED) != 0 : __any((gw & GEN16_RESTRICTED) != 0))
                     hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = s_win && hon_run && hit;
             }
@@ -780,7 +782,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 }
                 if (IPW == 1) oss = os;
                 for (uint32_t x = os; x; x &= x - 1) {
-                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (TS - 1);
+                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
                     if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
                     any_rows |= 1u << r;
                 }
@@ -874,9 +876,9 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i]; gp(P.mgen)[mb + i] = s_gen[i]; }
+            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i]; gp(P.mgen)[mb + i] = gen32(s_gen[i]); }
         }
-        for (uint32_t i = lane; i < TS * nkw; i += 64) gp(P.act)[item * TS * nkw + i] = s_act[i];
+        for (uint32_t i = lane; i < RS * nkw; i += 64) gp(P.act)[item * RS * nkw + i] = s_act[i];
     }
     if (lane == 0) {
         gp(P.actany)[item] = any_rows;

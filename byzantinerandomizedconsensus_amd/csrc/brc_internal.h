@@ -98,7 +98,8 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
 // meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 | consensus area |
-// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 | klist[NK] u32 | red[12] u32
+// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 | klist[NK] u32 | red[12] u32 |
+// pmw[2][CHUNK_W][NW] u32
 // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32 (one key variant per origin)
 __host__ __device__ inline uint32_t cons_words_wide(bool spec, uint32_t npad, uint32_t Q) {
     const uint32_t nw = npad / 64;
@@ -108,7 +109,7 @@ __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32
     const uint32_t nw = (uint32_t)npad / 64;
     return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
                 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
-           4 * (NK + NK + 12);
+           4 * (NK + NK + 12 + 2 * CHUNK_W * nw);
 }
 
 // Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of

@@ -45,6 +45,10 @@ template <int NPAD, int DM, bool EV, int MODE>
 __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
+    // DM > 8 (geometric): in a given wave most delays carry no send, so each wave publishes which
+    // did (pmw) and the readers visit only those; with DM <= 8 that bookkeeping costs more than it
+    // saves (measured cfg5: geometric -20% kernel time, const/uniform +5%)
+    constexpr bool SPARSE_D = DM > 8;
     constexpr int NW = NPAD / 64;
     constexpr int NPL = DM == 4 ? 2 : DM == 8 ? 3 : 4;   // bit planes of a link's delay code
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del, model = P.delay_model;
     // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 |
     //   consensus area | xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
-    //   klist[NK] u32 | red[3][4] u32
+    //   klist[NK] u32 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
     // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32
     uint64_t* s_meta = smem;
     uint64_t* s_act = s_meta + NK;
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     uint32_t* s_gen = (uint32_t*)(s_outm + 16 * NW);
     uint32_t* s_klist = s_gen + NK;
     uint32_t* s_red = s_klist + NK;
-
+    uint32_t* s_pmw = s_red + 12;                // per wave: delays (compact index) with any send
     const uint32_t d = (uint32_t)tid;
     const uint64_t g = P.inst_offset + inst;
     auto validw = [&](int w) -> uint64_t {     // senders < n in word w
@@ -196,6 +200,13 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         if (real && ((s_outm[i * NW + wid] >> lane) & 1ull)) outset |= 1u << i;
     }
     dset = uni32(dset);
+    // dlist: the delays present, minus one, 4 bits each in ascending order (compact index j)
+    uint64_t dlist = 0;
+    {
+        uint32_t nd = 0;
+        for (uint32_t ds = dset; ds; ds &= ds - 1) dlist |= (uint64_t)(__ffs(ds) - 1) << (4 * nd++);
+    }
+    dlist = uni64(dlist);
     const uint32_t maxout = hibit(outset);
     bool ovf = (uint32_t)__popc(dset) > nL, badinj = false;   // cannot happen: delay_values() bounds dset
     const gptr_t<uint64_t> mycells = gp(P.cells) + inst * (uint64_t)NK * NPAD + d;   // cell (k, d) at [k * NPAD]
@@ -495,12 +506,18 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
                     uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
-                    uint32_t j = 0;
+                    uint32_t j = 0, pm = 0;
                     for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
                         const uint32_t dly = (uint32_t)__ffs(ds);
                         const uint64_t be = __ballot(dE == dly), br = __ballot(dR == dly);
-                        if (lane == 0) { xb[j * 2 * NW + wid] = be; xb[j * 2 * NW + NW + wid] = br; }
+                        if constexpr (SPARSE_D) {
+                            if (be | br) {
+                                pm |= 1u << j;
+                                if (lane == 0) { xb[j * 2 * NW + wid] = be; xb[j * 2 * NW + NW + wid] = br; }
+                            }
+                        } else if (lane == 0) { xb[j * 2 * NW + wid] = be; xb[j * 2 * NW + NW + wid] = br; }
                     }
+                    if constexpr (SPARSE_D) { if (lane == 0) s_pmw[(buf * CHUNK_W + c) * NW + wid] = pm; }
                 }
             });
         };
@@ -512,7 +529,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             });
         };
         // phase 2: one (receiver d, key k) cell
-        auto process = [&](const uint32_t k, const uint64_t wd, uint32_t buf, int c) {
+        auto process = [&](const uint32_t k, const uint64_t wd, uint32_t buf, int c) __attribute__((always_inline)) {
             const uint64_t m = uni64(s_meta[k]);
             const uint32_t gw = uni32(s_gen[k]);
             const uint32_t gen = gw & GEN_MASK_W;
@@ -522,20 +539,39 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
             uint32_t ea = 0, ra = 0;
             {
+                // only the delays at which some wave had a send (each wave's pmw word); a wave that
+                // had none there did not write its ballot words, so they read as zero
                 const uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
-                uint32_t j = 0;
-                for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
-                    const uint32_t dly = (uint32_t)__ffs(ds);
-                    uint64_t xe[NW], xr[NW], any = 0;
+                if constexpr (SPARSE_D) {
+                    uint32_t pwv[NW], pm = 0;
 #pragma unroll
-                    for (int w = 0; w < NW; ++w) { xe[w] = xb[j * 2 * NW + w]; xr[w] = xb[j * 2 * NW + NW + w]; any |= xe[w] | xr[w]; }
-                    if (any) {
+                    for (int w = 0; w < NW; ++w) { pwv[w] = uni32(s_pmw[(buf * CHUNK_W + c) * NW + w]); pm |= pwv[w]; }
+                    for (; pm; pm &= pm - 1) {
+                        const uint32_t j = (uint32_t)__ffs(pm) - 1, dly = (uint32_t)((dlist >> (4 * j)) & 15u) + 1u;
                         Unrolled<NW>::run([&](auto wc) {
                             constexpr int w = decltype(wc)::value;
+                            const bool wrote = (pwv[w] >> j) & 1u;
+                            const uint64_t xe = wrote ? xb[j * 2 * NW + w] : 0ull, xr = wrote ? xb[j * 2 * NW + NW + w] : 0ull;
                             const uint64_t L = Lw(dly, wc);
-                            ea += (uint32_t)__popcll(xe[w] & L);
-                            ra += (uint32_t)__popcll(xr[w] & L);
+                            ea += (uint32_t)__popcll(xe & L);
+                            ra += (uint32_t)__popcll(xr & L);
                         });
+                    }
+                } else {
+                    uint32_t j = 0;
+                    for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
+                        const uint32_t dly = (uint32_t)__ffs(ds);
+                        uint64_t xe[NW], xr[NW], any = 0;
+#pragma unroll
+                        for (int w = 0; w < NW; ++w) { xe[w] = xb[j * 2 * NW + w]; xr[w] = xb[j * 2 * NW + NW + w]; any |= xe[w] | xr[w]; }
+                        if (any) {
+                            Unrolled<NW>::run([&](auto wc) {
+                                constexpr int w = decltype(wc)::value;
+                                const uint64_t L = Lw(dly, wc);
+                                ea += (uint32_t)__popcll(xe[w] & L);
+                                ra += (uint32_t)__popcll(xr[w] & L);
+                            });
+                        }
                     }
                 }
             }

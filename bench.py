@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--round-cap", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="collective backend for N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo "
+                         "only rehearses the multi-rank flow with several ranks sharing one GPU")
     return ap.parse_args()
 
 
@@ -107,11 +110,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    coll_dev = "cuda"
     if world > 1:
         import torch
         import torch.distributed as tdist
+        if args.backend == "gloo":                  # rehearsal: ranks may share a GPU
+            local %= torch.cuda.device_count()
+            coll_dev = "cpu"
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        if args.backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group("gloo")
         dist = tdist
 
     from byzantinerandomizedconsensus_amd import _lib as L
@@ -152,9 +162,9 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(kms) / len(kms)
     # the only collective: statistics (RCCL over xGMI), max of the wall clocks
-    st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(66))
-    elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
-    kernel_ms = shard.max_over_ranks(kernel_ms, dist, device="cuda")
+    st, hist = shard.reduce_stats(eng.stats(), dist, device=coll_dev, hist=eng.round_histogram(66))
+    elapsed = shard.max_over_ranks(elapsed, dist, device=coll_dev)
+    kernel_ms = shard.max_over_ranks(kernel_ms, dist, device=coll_dev)
     decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
     bad = st["overflow"] + st["stepcap"] + st["running"]
     if bad:
@@ -185,7 +195,7 @@ def main():
                        "mode": args.mode, "key_window": args.key_window,
                        "parallelism": "instance-sharded x%d" % world},
             "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
-            "replica_message_steps_per_s": arrivals * args.steps / world * world / elapsed,
+            "replica_message_steps_per_s": arrivals * args.steps / elapsed,
             "decided_fraction": decided / float(per * world),
             "kernel_ms": kernel_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -194,7 +204,7 @@ def main():
                                  % (SURVEY_BYTES_PER_CELL_STEP, cell_steps // world)},
         }
     eng.close()
-    if rank == 0 and not args.no_cpu and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:     # N = 1 only
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.mode, args.key_window, args.round_cap)
     if rank == 0:
         print(json.dumps(out))

@@ -1,0 +1,128 @@
+#!/usr/bin/env python3
+"""Throughput of every BASELINE.json configuration that runs on the GPU (configs[1..4]), one
+JSON line per workload.  bench.py stays the headline (cfg4); this measures the others with the
+same clock discipline so DESIGN.md can quote all of them.
+
+    python configs.py [--only cfg2,cfg3,...] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... configs.py
+        (cfg2 / cfg3 keep their TOTAL size and shard it; cfg4 / cfg5 are per GPU)
+
+Workloads:
+  cfg2       10,000 instances n=4 f=1, honest, uniform delays [1,4], reference protocol
+  cfg3       1,000,000 instances n=16 f=5, Byzantine {11..15} equivocating, uniform delays [1,4]
+  cfg4-ref   2^20 instances per GPU n=64 f=21, slow-set delays D=8 (the bench.py workload)
+  cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^19 instances per GPU
+  cfg5-*     n=256 f=85 SPEC, 2048 instances per GPU, const / uniform[1,4] / geometric<=16
+
+A step is one pass of the hot path over the batch (reset + run to completion); the timed region
+is K steps between barriers, max over ranks.  `roofline.achieved` = SURVEY §8(d)'s algorithmic
+6*ceil(n/8)+2 B per cell-step x cell-steps per launch / kernel time.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0
+COIN_SEED = 0xC017C017
+
+
+def workloads(L):
+    """name -> (instances, per_gpu, Engine kwargs)"""
+    uni, slow = L.DELAY_UNIFORM, L.DELAY_SLOWSET
+    base = dict(protocol="consensus", step_cap=4000, proposals=L.PROPOSALS_PHILOX, delay_const=1)
+    W = {
+        "cfg2": (10000, False, dict(base, n=4, f=1, seed=0x5EED0002, delay_model=uni, delay_max=4, round_cap=1,
+                                    key_window=8)),
+        "cfg3": (1000000, False, dict(base, n=16, f=5, seed=0x5EED0003, delay_model=uni, delay_max=4, round_cap=1,
+                                      key_window=4, variants=2, byz_pattern=L.BYZ_EQUIVOCATE,
+                                      byzantine=list(range(11, 16)))),
+        "cfg4-ref": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                         round_cap=1, key_window=4)),
+        "cfg4-spec": (1 << 19, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                          round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
+    }
+    for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
+        W["cfg5-" + name] = (2048, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
+                                             delay_max=dmax, round_cap=1, key_window=8, mode=L.MODE_SPEC,
+                                             coin_seed=COIN_SEED))
+    return W
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+    from byzantinerandomizedconsensus_amd import _lib as L
+    from byzantinerandomizedconsensus_amd import shard
+    from byzantinerandomizedconsensus_amd.engine import Engine
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    W = workloads(L)
+    names = [x for x in args.only.split(",") if x] or list(W)
+    for name in names:
+        size, per_gpu, kw = W[name]
+        first, count = shard.shard_range(size * world if per_gpu else size, world, rank)
+        n = kw["n"]
+        bpc = 6 * ((n + 7) // 8) + 2
+        with Engine(instances=count, instance_offset=first, device=local, **kw) as eng:
+            for _ in range(args.warmup):
+                eng.reset()
+                eng.run()
+            barrier()
+            t0 = time.perf_counter()
+            kms = []
+            for _ in range(args.steps):
+                eng.reset()
+                eng.run()
+                kms.append(eng.last_kernel_ms())
+            barrier()
+            elapsed = time.perf_counter() - t0
+            st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(66))
+        elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
+        kernel_ms = shard.max_over_ranks(sum(kms) / len(kms), dist, device="cuda")
+        if rank == 0:
+            achieved = bpc * (st["cell_steps"] / world) / (kernel_ms / 1e3) / 1e9
+            print(json.dumps({
+                "workload": name, "n": n, "f": kw["f"], "instances": st["instances"], "n_gpus": world,
+                "mode": "spec" if kw.get("mode") == L.MODE_SPEC else "reference",
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+                "kernel_ms": kernel_ms,
+                "decided_instances_per_s": st["decided"] * args.steps / elapsed,
+                "instances_per_s": st["instances"] * args.steps / elapsed,
+                "replica_message_steps_per_s": st["arrivals"] * args.steps / elapsed,
+                "statuses": {k: st[k] for k in ("done", "quiescent", "stepcap", "overflow", "running")},
+                "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
+                "cell_steps_per_launch": st["cell_steps"], "lane_loads_per_launch": st["lane_loads"],
+                "roofline": {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": achieved,
+                             "frac": achieved / HBM_PEAK_GBS,
+                             "note": "algorithmic %d B per cell-step (SURVEY 8(d) at n=%d)" % (bpc, n)},
+            }), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

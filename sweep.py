@@ -50,7 +50,7 @@ def main():
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl")
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         dist = tdist
     from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd import shard

@@ -324,7 +324,8 @@ int brc_create(const brc_config* cfg, void** out) {
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
-    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, nL, spec, c.key_window)
+    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xwords_wide(c.delay_model, c.delay_max, e->dm),
+                                            spec, c.key_window)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window, c.variants, e->rs) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {

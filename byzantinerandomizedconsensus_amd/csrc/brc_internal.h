@@ -105,6 +105,18 @@ __host__ __device__ inline uint32_t cons_words_wide(bool spec, uint32_t npad, ui
     const uint32_t nw = npad / 64;
     return spec ? (Q * npad + 1) / 2 : 4 * nw * npad;
 }
+// Wide kernel: link-delay code bit planes per DM (delay - 1 in NPL bits), and the u64 words one
+// wave publishes per (key, message type) in the ballot exchange: one per link delay present
+// (constant, slow-set), or -- uniform / geometric delays -- the NPL bit planes of "steps since
+// this lane sent, minus one" plus the mask of lanes whose send lies inside the 2^NPL window.
+__host__ __device__ constexpr int npl_of(int dm) { return dm == 4 ? 2 : dm == 8 ? 3 : 4; }
+__host__ __device__ inline bool plane_model(uint32_t model) {
+    return model == BRC_DELAY_UNIFORM || model == BRC_DELAY_GEOMETRIC;
+}
+__host__ __device__ inline uint32_t xwords_wide(uint32_t model, uint32_t dmax, int dm) {
+    return plane_model(model) ? (uint32_t)npl_of(dm) + 1u : delay_values(model, dmax);
+}
+
 __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec, uint32_t Q) {
     const uint32_t nw = (uint32_t)npad / 64;
     return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +

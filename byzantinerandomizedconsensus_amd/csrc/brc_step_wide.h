@@ -50,7 +50,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     // saves (measured cfg5: geometric -20% kernel time, const/uniform +5%)
     constexpr bool SPARSE_D = DM > 8;
     constexpr int NW = NPAD / 64;
-    constexpr int NPL = DM == 4 ? 2 : DM == 8 ? 3 : 4;   // bit planes of a link's delay code
+    constexpr int NPL = npl_of(DM);                      // bit planes of a link's delay code
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
     const int tid = threadIdx.x, wid = tid / 64, lane = tid % 64;
@@ -58,8 +58,12 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     if (inst >= P.instances) return;            // whole workgroup exits
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw, nL = P.nL;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del, model = P.delay_model;
+    // uniform / geometric delays: arrivals are matched on delay-code bit planes (xwords_wide), so
+    // the exchange and the receiver's test cost the same however many delays are present
+    const bool planes = plane_model(model);
+    const uint32_t nX = planes ? (uint32_t)NPL + 1u : nL;   // exchanged words per (key, type)
     // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 |
-    //   consensus area | xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
+    //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
     //   klist[NK] u32 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
     // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32
     uint64_t* s_meta = smem;
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     // most once and the origin count needs no host set.
     uint32_t* s_cnt = (uint32_t*)s_hm;
     uint64_t* s_xb = s_hm + cons_words_wide(SPEC, NPAD, Q);
-    uint64_t* s_outm = s_xb + 2 * CHUNK_W * nL * 2 * NW;
+    uint64_t* s_outm = s_xb + 2 * CHUNK_W * nX * 2 * NW;
     uint32_t* s_gen = (uint32_t*)(s_outm + 16 * NW);
     uint32_t* s_klist = s_gen + NK;
     uint32_t* s_red = s_klist + NK;
@@ -505,7 +509,20 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                     const bool cur = m_s1(m) != 0 && real && (((uint32_t)ww[c] >> 21) & GEN_MASK_W) == gen;
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
-                    uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
+                    uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nX) * 2 * NW;
+                    if (planes) {
+                        // code = steps since this lane sent - 1; a receiver matches it against the
+                        // code of its link from this lane, plane by plane
+                        const uint32_t cE = dE - 1u, cR = dR - 1u;
+                        const uint64_t vE = __ballot(cE < (1u << NPL)), vR = __ballot(cR < (1u << NPL));
+                        if (lane == 0) { xb[NPL * 2 * NW + wid] = vE; xb[NPL * 2 * NW + NW + wid] = vR; }
+#pragma unroll
+                        for (int b = 0; b < NPL; ++b) {
+                            const uint64_t be = __ballot((cE >> b) & 1u), br = __ballot((cR >> b) & 1u);
+                            if (lane == 0) { xb[b * 2 * NW + wid] = be; xb[b * 2 * NW + NW + wid] = br; }
+                        }
+                        return;
+                    }
                     uint32_t j = 0, pm = 0;
                     for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
                         const uint32_t dly = (uint32_t)__ffs(ds);
@@ -541,8 +558,23 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             {
                 // only the delays at which some wave had a send (each wave's pmw word); a wave that
                 // had none there did not write its ballot words, so they read as zero
-                const uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nL) * 2 * NW;
-                if constexpr (SPARSE_D) {
+                const uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nX) * 2 * NW;
+                if (planes) {
+                    // senders whose send is `code + 1` steps old, where code is their link's delay
+                    // code to this receiver: no plane differs (PL = 0 off the real receivers,
+                    // whose counts are never used)
+                    Unrolled<NW>::run([&](auto wc) {
+                        constexpr int w = decltype(wc)::value;
+                        uint64_t xe = 0, xr = 0;
+#pragma unroll
+                        for (int b = 0; b < NPL; ++b) {
+                            xe |= xb[b * 2 * NW + w] ^ PL[b][w];
+                            xr |= xb[b * 2 * NW + NW + w] ^ PL[b][w];
+                        }
+                        ea += (uint32_t)__popcll(xb[NPL * 2 * NW + w] & ~xe);
+                        ra += (uint32_t)__popcll(xb[NPL * 2 * NW + NW + w] & ~xr);
+                    });
+                } else if constexpr (SPARSE_D) {
                     uint32_t pwv[NW], pm = 0;
 #pragma unroll
                     for (int w = 0; w < NW; ++w) { pwv[w] = uni32(s_pmw[(buf * CHUNK_W + c) * NW + w]); pm |= pwv[w]; }

@@ -10,6 +10,7 @@ same clock discipline so DESIGN.md can quote all of them.
 Workloads:
   cfg2       10,000 instances n=4 f=1, honest, uniform delays [1,4], reference protocol
   cfg3       1,000,000 instances n=16 f=5, Byzantine {11..15} equivocating, uniform delays [1,4]
+  cfg2-spec, cfg3-spec   the same two in SPEC mode (the reference protocol stalls on most of them)
   cfg4-ref   2^20 instances per GPU n=64 f=21, slow-set delays D=8 (the bench.py workload)
   cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^19 instances per GPU
   cfg5-*     n=256 f=85 SPEC, 2048 instances per GPU, const / uniform[1,4] / geometric<=16
@@ -41,6 +42,13 @@ def workloads(L):
         "cfg3": (1000000, False, dict(base, n=16, f=5, seed=0x5EED0003, delay_model=uni, delay_max=4, round_cap=1,
                                       key_window=4, variants=2, byz_pattern=L.BYZ_EQUIVOCATE,
                                       byzantine=list(range(11, 16)))),
+        # the reference protocol stalls on most cfg2 / cfg3 instances (an early ECHO blocks the SEND,
+        # SURVEY K2); the intended protocol terminates on all of them
+        "cfg2-spec": (10000, False, dict(base, n=4, f=1, seed=0x5EED0002, delay_model=uni, delay_max=4,
+                                         round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
+        "cfg3-spec": (1000000, False, dict(base, n=16, f=5, seed=0x5EED0003, delay_model=uni, delay_max=4,
+                                           round_cap=1, key_window=4, variants=2, byz_pattern=L.BYZ_EQUIVOCATE,
+                                           byzantine=list(range(11, 16)), mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
         "cfg4-ref": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                          round_cap=1, key_window=4)),
         "cfg4-spec": (1 << 19, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,

@@ -672,15 +672,21 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         }
         if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK]) {     // p < nkeys + CHUNK: padded list
+        // p < nkeys + CHUNK: padded list.  The key ids stay in SGPRs with the words they address,
+        // so processing a key does not wait on another LDS round trip for its id.
+        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK], uint32_t (&kk)[CHUNK]) {
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
-                ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * (CW * 64)];
+                kk[c] = uni32(s_klist[p + c]);
+                ww[c] = mycells[(size_t)kk[c] * (CW * 64)];
             });
         };
         auto process = [&](const uint32_t k, const uint64_t wd) {
-            uint64_t m = s_meta[mbase + k];                      // (k == NK, the trash row: junk, unused)
-            uint32_t gw = s_gen[mbase + k];
+            // both LDS reads issue before either is waited on (k == NK, the trash row: junk, unused)
+            const uint64_t m_raw = s_meta[mbase + k];
+            const uint32_t gw_raw = s_gen[mbase + k];
+            uint64_t m = m_raw;
+            uint32_t gw = gw_raw;
             if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
             const uint32_t gen = gw & GEN_MASK;
             const bool kl = k < NK && m_s1(m) != 0;              // the slot holds a key
@@ -795,17 +801,20 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         };
         {
             uint64_t wA[CHUNK];
-            fetch(0, wA);
+            uint32_t kA[CHUNK];
+            fetch(0, wA, kA);
             for (uint32_t p = 0; p < nkeys; p += CHUNK) {
                 uint64_t wB[CHUNK];
-                fetch(p + CHUNK, wB);
+                uint32_t kB[CHUNK];
+                fetch(p + CHUNK, wB, kB);
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    process(uni32(s_klist[p + c]), wA[c]);       // padding slots: the trash row
+                    process(kA[c], wA[c]);                       // padding slots: the trash row
                 });
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     wA[c] = wB[c];
+                    kA[c] = kB[c];
                 });
             }
         }

@@ -499,13 +499,18 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         __syncthreads();
 
         // phase 1 of a chunk: ballot words "my ECHO / READY of key c was sent dly steps ago"
-        auto ballots = [&](uint32_t p, uint32_t buf, const uint64_t (&ww)[CHUNK_W]) {
+        // The key id, meta word and generation it reads stay in SGPRs for phase 2 (process): meta
+        // changes in between only in t_quiet, through process's own atomicMax, which keeps the max.
+        auto ballots = [&](uint32_t p, uint32_t buf, const uint64_t (&ww)[CHUNK_W], const uint32_t (&kk)[CHUNK_W],
+                           uint64_t (&mm)[CHUNK_W], uint32_t (&gg)[CHUNK_W]) {
             Unrolled<CHUNK_W>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 if (p + c < nkeys) {
-                    const uint32_t k = uni32(s_klist[p + c]);
+                    const uint32_t k = kk[c];
                     const uint64_t m = uni64(s_meta[k]);
-                    const uint32_t gen = uni32(s_gen[k]) & GEN_MASK_W;
+                    const uint32_t gw = uni32(s_gen[k]);
+                    mm[c] = m; gg[c] = gw;
+                    const uint32_t gen = gw & GEN_MASK_W;
                     const bool cur = m_s1(m) != 0 && real && (((uint32_t)ww[c] >> 21) & GEN_MASK_W) == gen;
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
@@ -538,17 +543,20 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                 }
             });
         };
-        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK_W]) {
+        auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK_W], uint32_t (&kk)[CHUNK_W]) {
             Unrolled<CHUNK_W>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 ww[c] = TIMES_NEVER;
-                if (p + c < nkeys) ww[c] = mycells[(size_t)uni32(s_klist[p + c]) * NPAD];
+                kk[c] = 0;
+                if (p + c < nkeys) {
+                    kk[c] = uni32(s_klist[p + c]);
+                    ww[c] = mycells[(size_t)kk[c] * NPAD];
+                }
             });
         };
         // phase 2: one (receiver d, key k) cell
-        auto process = [&](const uint32_t k, const uint64_t wd, uint32_t buf, int c) __attribute__((always_inline)) {
-            const uint64_t m = uni64(s_meta[k]);
-            const uint32_t gw = uni32(s_gen[k]);
+        auto process = [&](const uint32_t k, const uint64_t wd, const uint64_t m, const uint32_t gw, uint32_t buf, int c)
+            __attribute__((always_inline)) {
             const uint32_t gen = gw & GEN_MASK_W;
             const bool kl = m_s1(m) != 0;                        // the slot holds a key
             const bool cur = kl && real && (((uint32_t)wd >> 21) & GEN_MASK_W) == gen;
@@ -658,20 +666,25 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         };
         {
             uint64_t wA[CHUNK_W];
-            fetch(0, wA);
+            uint32_t kA[CHUNK_W];
+            fetch(0, wA, kA);
             for (uint32_t p = 0; p < nkeys; p += CHUNK_W) {
                 const uint32_t buf = (p / CHUNK_W) & 1;
-                ballots(p, buf, wA);
+                uint64_t mA[CHUNK_W];
+                uint32_t gA[CHUNK_W];
+                ballots(p, buf, wA, kA, mA, gA);
                 __syncthreads();
                 uint64_t wB[CHUNK_W];
-                fetch(p + CHUNK_W, wB);
+                uint32_t kB[CHUNK_W];
+                fetch(p + CHUNK_W, wB, kB);
                 Unrolled<CHUNK_W>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    if (p + c < nkeys) process(uni32(s_klist[p + c]), wA[c], buf, c);
+                    if (p + c < nkeys) process(kA[c], wA[c], mA[c], gA[c], buf, c);
                 });
                 Unrolled<CHUNK_W>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     wA[c] = wB[c];
+                    kA[c] = kB[c];
                 });
             }
         }

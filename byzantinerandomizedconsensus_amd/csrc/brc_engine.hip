@@ -109,6 +109,7 @@ struct Engine {
     brc_config cfg;
     int npad = 0, dm = 0, ipw = 0, nkw_t = 0;
     bool wide = false;                           // n > 64: one workgroup per instance (brc_step_wide.h)
+    bool regmask = false;                        // NPAD = 64 lean kernel with register delay masks (NLR = 2)
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
@@ -324,9 +325,11 @@ int brc_create(const brc_config* cfg, void** out) {
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
+    e->regmask = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && nL <= 2;
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xwords_wide(c.delay_model, c.delay_max, e->dm),
                                             spec, c.key_window)
-                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, nL, spec, c.key_window, c.variants, e->rs) * WPB;
+                           : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
+                                                c.variants, e->rs) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
@@ -517,8 +520,9 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
     const int kmode = c.peer_mode == BRC_PEER_CONNECTION ? KMODE_CONN : (int)c.mode;
-    rc = launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
-                     e->dparams);
+    rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)
+                    : launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
+                                  e->dparams);
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));

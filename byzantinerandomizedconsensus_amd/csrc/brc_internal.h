@@ -137,6 +137,8 @@ int launch_step_8(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, 
 int launch_step_16(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 int launch_step_32(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 int launch_step_64(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+// NPAD = 64 lean kernels with the (at most two) link-delay masks in registers (brc_kern_64r.hip)
+int launch_step_64r(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 // wide kernel (brc_step_wide.h): one workgroup of NPAD threads per instance
 int launch_step_128(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 int launch_step_256(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);

@@ -1,0 +1,10 @@
+// brc_kern_64r.hip -- lean step-kernel instantiations for NPAD = 64 with register-resident link-delay
+// masks (NLR = 2: constant and slow-set delay models); own translation unit so the build compiles
+// it beside brc_kern_64.hip (see brc_step.h).
+#include "brc_step.h"
+
+namespace brc {
+int launch_step_64r(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    return launch_step_regmask(dm, events, mode, blocks, lds, s, P);
+}
+}  // namespace brc

@@ -233,14 +233,26 @@ __device__ __forceinline__ uint64_t ring_put(uint64_t ring, uint32_t tl, uint32_
 #ifndef BRC_MIN_WAVES
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
+#ifndef BRC_MIN_WAVES_LEAN
+#define BRC_MIN_WAVES_LEAN 5 // ... for the one-instance-per-wave (lean) instantiations
+#endif
 
-template <int NPAD, int DM, bool EV, int MODE>
-__global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params* pp) {
+// Lean instantiations: one instance per wave (NPAD = 64, IPW = 1) with sender-identity peers.
+// Every key-slot field is then wave-uniform, so the per-key work runs on scalar key ids,
+// metadata read once per chunk, exec-masked cell stores and (NLR = 2) link-delay masks held in
+// registers -- the headline configuration has exactly two link delays.
+template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
+
+template <int NPAD, int DM, bool EV, int MODE, int NLR>
+__global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? BRC_MIN_WAVES_LEAN : BRC_MIN_WAVES))
+void brc_step(const Params* pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
     // pinning ~60 of them in SGPRs across the hot loop.  Hot fields are copied to locals below.
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
+    constexpr bool LEAN = lean_kernel<NPAD, MODE>();
+    static_assert(NLR == 0 || (LEAN && NLR == 2), "register delay masks: lean kernels, two delays");
     constexpr uint32_t CW = CONN ? 3 : 1;        // u64 words per cell (CONN: + ECHO and READY send rings)
     using T = typename MaskOf<NPAD>::type;
     constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
@@ -255,7 +267,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
     //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16
     // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
-    const uint32_t nL = P.nL;
+    const uint32_t nL = NLR ? 0u : P.nL;        // NLR: the masks live in registers, not in LDS
     const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
     const bool seen_on = NV > 1;                 // SPEC: host sets needed only with key variants
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     const uint32_t mbase = seg * NK;             // this lane's instance in the LDS meta arrays
 
     ItemState its = P.items[item];
-    uint32_t t = its.t, inj_pos = its.inj_pos;
+    uint32_t t = LEAN ? uni32(its.t) : its.t, inj_pos = LEAN ? uni32(its.inj_pos) : its.inj_pos;   // lean: wave-uniform
     const uint32_t inj_off = gp(P.inj_off)[item], inj_cnt = gp(P.inj_cnt)[item];
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
@@ -360,13 +372,34 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     dlist = uni64(dlist); ndl = uni32(ndl);
     // compact delay masks: the j-th delay present in the wave -> s_L[j]; every nonzero L[i] of an
     // honest receiver is in dset (its sender's outset has bit i)
-    {
+    // NLR: the (at most two) delays present -> registers: RL0/RL1 = masks, dly0/dly1 = delays,
+    // OV0/OV1 = the wave's senders with such a link (wave-uniform)
+    T RL0 = 0, RL1 = 0;
+    uint32_t dly0 = 0, dly1 = 0;
+    uint64_t OV0 = 0, OV1 = 0;
+    if constexpr (NLR != 0) {
+        if (ndl > 2) ovf = true;                     // cannot happen: the host picks NLR for <= 2 delays
+        dly0 = ndl > 0 ? (uint32_t)(dlist & 15) + 1u : 0u;
+        dly1 = ndl > 1 ? (uint32_t)((dlist >> 4) & 15) + 1u : 0u;
+#pragma unroll
+        for (int i = 0; i < DM; ++i) {
+            if ((uint32_t)i + 1 == dly0) RL0 = L[i];
+            if ((uint32_t)i + 1 == dly1) RL1 = L[i];
+        }
+        if (ndl > 0) OV0 = uni64(readlane64(outv, (int)dly0 - 1));
+        if (ndl > 1) OV1 = uni64(readlane64(outv, (int)dly1 - 1));
+    } else {
         uint32_t j = 0;
 #pragma unroll
         for (int i = 0; i < DM; ++i)
             if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
+    // the j-th delay mask present in the wave (j < ndl)
+    auto Lmask = [&](uint32_t j) -> T {
+        if constexpr (NLR != 0) return j == 0 ? RL0 : RL1;
+        else return s_L[j * 64 + lane];
+    };
     // cell (k, lane) at [k * CW * 64] (+ 64, + 128: CONN send rings)
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
 
@@ -391,6 +424,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
 
     uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
+    uint32_t st_bcast = 0;                       // lean path: ECHO/READY broadcasts (n messages each)
 
     auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b, uint32_t v) {
         if (EV) {
@@ -544,7 +578,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 if (is_send && mine && honest && ((r.dst >> d) & 1ull)) {
                     uint32_t j = 0;
                     for (uint32_t ds = dset; ds; ds &= ds - 1, ++j)
-                        if ((s_L[j * 64 + lane] >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
+                        if ((Lmask(j) >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
                 }
                 const uint32_t os = wave_or(myset);
                 if (mine) {
@@ -655,7 +689,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
         if (inj_pos < inj_cnt) next = min(next, gp(P.inj)[inj_off + inj_pos].t);
         if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
         if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
-        t = next;
+        t = LEAN ? uni32(next) : next;
         const uint32_t row = t & (RS - 1);
 
         // ================= BRB: the step's active key slots; one (receiver, key) cell per lane.
@@ -680,6 +714,111 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 kk[c] = uni32(s_klist[p + c]);
                 ww[c] = mycells[(size_t)kk[c] * (CW * 64)];
             });
+        };
+        // ---- lean path (IPW == 1): k, m (meta), gw (generation) are wave-uniform; wd = this lane's
+        // cell word.  Same transitions as process() below, with the per-key work cut down:
+        // arrivals are matched against precomputed t - delay, the delay masks are registers
+        // (NLR), and only lanes whose cell changes store (exec-masked).
+        const uint32_t tm0 = t - dly0, tm1 = t - dly1;
+        const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
+        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd) {
+            const uint32_t gen = gw & GEN_MASK;
+            const bool kl = k < NK && m_s1(m) != 0;              // the slot holds a key
+            const uint32_t wlo = (uint32_t)wd, whi = (uint32_t)(wd >> 32);
+            const bool cur = kl && real && (wlo >> 19) == gen;   // gen: bits 19..31
+            const uint32_t lo = cur ? wlo : 0u, hi = cur ? whi : 0xFFFFFFFFu;
+            const uint32_t tE = hi & 0xFFFF, tR = hi >> 16;      // steps this lane SENT ECHO / READY
+            uint32_t ea = 0, ra = 0;
+            if constexpr (NLR != 0) {
+                const uint64_t be = __ballot(tE == tm0), br = __ballot(tR == tm0);
+                ea = popc(be & RL0);
+                ra = popc(br & RL0);
+                if (ndl > 1) {
+                    const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
+                    ea += popc(be1 & RL1);
+                    ra += popc(br1 & RL1);
+                }
+            } else {
+                const uint32_t dE = t - tE, dR = t - tR;
+                Unrolled<DM>::run([&](auto jc) {
+                    constexpr int j = decltype(jc)::value;
+                    if ((uint32_t)j < ndl) {
+                        const uint32_t dly = (dlist >> (4 * j)) & 15u;
+                        const uint64_t be = __ballot(dE == dly + 1u), br = __ballot(dR == dly + 1u);
+                        const T Lj = s_L[j * 64 + lane];
+                        ea += popc(be & Lj);
+                        ra += popc(br & Lj);
+                    }
+                });
+            }
+            // SEND from the key's origin: arrives at t_send + delay(origin -> d)
+            bool s_arr = false;
+            const uint32_t dt = t - m_tsend(m);
+            bool s_win;
+            uint32_t sj = 0;                                     // index of delay dt among those present
+            if constexpr (NLR != 0) {
+                s_win = kl && (dt == dly0 || (ndl > 1 && dt == dly1));
+                sj = dt == dly0 ? 0u : 1u;
+            } else {
+                s_win = kl && dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);
+                sj = popc(dset & ((1u << ((dt - 1u) & 31)) - 1u));
+            }
+            if (s_win) {
+                bool hit = (Lmask(sj) >> m_sender(m)) & 1;
+                if (gw & GEN16_RESTRICTED) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
+                s_arr = honest && hit;
+            }
+            const bool has = kl && honest && (s_arr || ea || ra);
+            st_loads += (kl && real) ? 1u : 0u;
+            uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
+            bool es, rs, dl;
+            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
+            else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
+            if (has) {   // lanes without arrivals keep their word: no store
+                const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
+                const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
+                (icells + (size_t)k * 64)[lane] = (uint64_t)nlo | ((uint64_t)nhi << 32);
+                st_arr += ea + ra + (s_arr ? 1u : 0u);
+                st_cells += 1u;
+            }
+            st_bcast += (es ? 1u : 0u) + (rs ? 1u : 0u);
+            if (__ballot(dl)) {
+                if (dl) {
+                    atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], 1ull << (k & 63));
+                    st_del += 1u;
+                }
+            }
+            if (EV) {
+                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
+            }
+            // sends: ring marks at t + every delay some sending lane has; t_quiet of the key
+            const uint64_t sb = __ballot(es || rs);
+            if (sb) {
+                uint32_t os = 0;
+                if constexpr (NLR != 0) {
+                    if (sb & OV0) os |= 1u << (dly0 - 1u);
+                    if (sb & OV1) os |= 1u << (dly1 - 1u);
+                } else {
+                    for (uint32_t ds = dset; ds; ds &= ds - 1) {
+                        const uint32_t i = (uint32_t)__ffs(ds) - 1;
+                        if (sb & readlane64(outv, (int)i)) os |= 1u << i;
+                    }
+                }
+                for (uint32_t x = os; x; x &= x - 1) {
+                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
+                    if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
+                    any_rows |= 1u << r;
+                }
+                const uint32_t myq = os ? t + hibit(os) : 0u;
+                if (kl && myq) {
+                    if (lane == 0 && myq > m_tquiet(m)) s_meta[k] = m_with_tquiet(m, myq);
+                    q_until = max(q_until, myq);
+                }
+            }
         };
         auto process = [&](const uint32_t k, const uint64_t wd) {
             // both LDS reads issue before either is waited on (k == NK, the trash row: junk, unused)
@@ -722,7 +861,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                     if ((uint32_t)j < ndl) {
                         const uint32_t dly = (dlist >> (4 * j)) & 15u;
                         const uint64_t be = __ballot(dE == dly + 1u), br = __ballot(dR == dly + 1u);
-                        const T Lj = s_L[j * 64 + lane];
+                        const T Lj = Lmask(j);
                         ea += popc((T)(be >> segbase) & Lj);
                         ra += popc((T)(br >> segbase) & Lj);
                     }
@@ -734,7 +873,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             const uint32_t bit = 1u << ((dt - 1u) & 31);
             const bool s_win = kl && dt - 1u < D && (dset & bit) != 0;     // uniform if IPW == 1
             if (IPW == 1 ? s_win : __any(s_win)) {
-                bool hit = (s_L[popc(dset & (bit - 1u)) * 64 + lane] >> m_sender(m)) & 1;
+                bool hit = (Lmask(popc(dset & (bit - 1u))) >> m_sender(m)) & 1;
                 if (IPW == 1 ? (gw & GEN16_RESTRICTED) != 0 : __any((gw & GEN16_RESTRICTED) != 0))
                     hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = s_win && hon_run && hit;
@@ -799,7 +938,37 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
                 }
             }
         };
-        {
+        if constexpr (LEAN) {
+            // software pipeline, unrolled by CHUNK so the in-flight cell words never move between
+            // registers: slot c holds key p + c; right after it is processed, slot c loads key
+            // p + c + CHUNK, so CHUNK cell loads stay in flight.  The chunk's key metadata is read
+            // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
+            // exact).  Slots past the list load the trash row NK and are not processed.
+            auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
+            auto cell = [&](uint32_t k) { return (icells + (size_t)k * 64)[lane]; };
+            uint64_t w[CHUNK];
+            uint32_t kk[CHUNK];
+            Unrolled<CHUNK>::run([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                kk[c] = kid(c);
+                w[c] = cell(kk[c]);
+            });
+            for (uint32_t p = 0; p < nkeys; p += CHUNK) {
+                uint64_t mm[CHUNK];
+                uint32_t gg[CHUNK];
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    mm[c] = s_meta[kk[c]];
+                    gg[c] = s_gen[kk[c]];
+                });
+                Unrolled<CHUNK>::run([&](auto ci) {
+                    constexpr int c = decltype(ci)::value;
+                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c]);
+                    kk[c] = kid(p + c + CHUNK);
+                    w[c] = cell(kk[c]);
+                });
+            }
+        } else {
             uint64_t wA[CHUNK];
             uint32_t kA[CHUNK];
             fetch(0, wA, kA);
@@ -910,6 +1079,7 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
             for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
         }
     }
+    st_msgs += st_bcast * n;
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
 #pragma unroll
@@ -944,10 +1114,10 @@ __global__ __launch_bounds__(64 * WPB, BRC_MIN_WAVES) void brc_step(const Params
     }
 }
 
-// Launch one (DM, EV, SPEC) instantiation of the step kernel for a fixed NPAD.
-template <int NPAD, int DMX, bool EV, int MODE>
+// Launch one (DM, EV, MODE, NLR) instantiation of the step kernel for a fixed NPAD.
+template <int NPAD, int DMX, bool EV, int MODE, int NLR = 0>
 int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step<NPAD, DMX, EV, MODE>;
+    auto kern = brc_step<NPAD, DMX, EV, MODE, NLR>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -968,6 +1138,26 @@ int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hi
         if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \
         if (mode == BRC_MODE_BEB) return events ? launch_one<NPAD, DMX, true, BRC_MODE_BEB>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_BEB>(blocks, lds, s, P); \
         return events ? launch_one<NPAD, DMX, true, BRC_MODE_REFERENCE>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_REFERENCE>(blocks, lds, s, P); \
+    }
+#ifdef BRC_ONLY_DM8
+    BRC_CASE(8)
+#else
+    BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
+#endif
+#undef BRC_CASE
+    return BRC_E_INVALID;
+}
+
+// Lean kernels with register-resident delay masks (NLR = 2): NPAD = 64, sender peers, at most two
+// distinct link delays (constant or slow-set models).
+inline int launch_step_regmask(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s,
+                               const Params* P) {
+    if (mode == KMODE_CONN) return BRC_E_INVALID;
+#define BRC_CASE(DMX)                                                                                  \
+    if (dm == DMX) {                                                                                   \
+        if (mode == BRC_MODE_SPEC) return events ? launch_one<64, DMX, true, BRC_MODE_SPEC, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_SPEC, 2>(blocks, lds, s, P); \
+        if (mode == BRC_MODE_BEB) return events ? launch_one<64, DMX, true, BRC_MODE_BEB, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_BEB, 2>(blocks, lds, s, P); \
+        return events ? launch_one<64, DMX, true, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P); \
     }
 #ifdef BRC_ONLY_DM8
     BRC_CASE(8)

@@ -425,6 +425,7 @@ void brc_step(const Params* pp) {
 
     uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
     uint32_t st_bcast = 0;                       // lean path: ECHO/READY broadcasts (n messages each)
+    uint32_t nk_lean = 0;                        // lean path: keys processed (wave-uniform)
 
     auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b, uint32_t v) {
         if (EV) {
@@ -723,20 +724,27 @@ void brc_step(const Params* pp) {
         const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
         auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd) {
             const uint32_t gen = gw & GEN_MASK;
-            const bool kl = k < NK && m_s1(m) != 0;              // the slot holds a key
+            if (m_s1(m) == 0) return;                            // the slot holds no key
+            ++nk_lean;                                           // lane loads: one word per real lane
             const uint32_t wlo = (uint32_t)wd, whi = (uint32_t)(wd >> 32);
-            const bool cur = kl && real && (wlo >> 19) == gen;   // gen: bits 19..31
+            // a stale word (older generation) is a fresh cell: lanes that are not real replicas
+            // and Byzantine lanes never store here, so their words read "never sent"
+            const bool cur = (wlo >> 19) == gen;                 // gen: bits 19..31
             const uint32_t lo = cur ? wlo : 0u, hi = cur ? whi : 0xFFFFFFFFu;
             const uint32_t tE = hi & 0xFFFF, tR = hi >> 16;      // steps this lane SENT ECHO / READY
+            // arrivals: senders whose message lands now, per delay present (empty ballots skipped)
             uint32_t ea = 0, ra = 0;
+            uint64_t be_any = 0, br_any = 0;
             if constexpr (NLR != 0) {
-                const uint64_t be = __ballot(tE == tm0), br = __ballot(tR == tm0);
-                ea = popc(be & RL0);
-                ra = popc(br & RL0);
+                const uint64_t be0 = __ballot(tE == tm0), br0 = __ballot(tR == tm0);
+                if (be0) ea = popc(be0 & RL0);
+                if (br0) ra = popc(br0 & RL0);
+                be_any = be0; br_any = br0;
                 if (ndl > 1) {
                     const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
-                    ea += popc(be1 & RL1);
-                    ra += popc(br1 & RL1);
+                    if (be1) ea += popc(be1 & RL1);
+                    if (br1) ra += popc(br1 & RL1);
+                    be_any |= be1; br_any |= br1;
                 }
             } else {
                 const uint32_t dE = t - tE, dR = t - tR;
@@ -745,9 +753,12 @@ void brc_step(const Params* pp) {
                     if ((uint32_t)j < ndl) {
                         const uint32_t dly = (dlist >> (4 * j)) & 15u;
                         const uint64_t be = __ballot(dE == dly + 1u), br = __ballot(dR == dly + 1u);
-                        const T Lj = s_L[j * 64 + lane];
-                        ea += popc(be & Lj);
-                        ra += popc(br & Lj);
+                        if (be | br) {
+                            const T Lj = s_L[j * 64 + lane];
+                            ea += popc(be & Lj);
+                            ra += popc(br & Lj);
+                        }
+                        be_any |= be; br_any |= br;
                     }
                 });
             }
@@ -757,10 +768,10 @@ void brc_step(const Params* pp) {
             bool s_win;
             uint32_t sj = 0;                                     // index of delay dt among those present
             if constexpr (NLR != 0) {
-                s_win = kl && (dt == dly0 || (ndl > 1 && dt == dly1));
+                s_win = dt == dly0 || (ndl > 1 && dt == dly1);
                 sj = dt == dly0 ? 0u : 1u;
             } else {
-                s_win = kl && dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);
+                s_win = dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);
                 sj = popc(dset & ((1u << ((dt - 1u) & 31)) - 1u));
             }
             if (s_win) {
@@ -768,21 +779,60 @@ void brc_step(const Params* pp) {
                 if (gw & GEN16_RESTRICTED) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = honest && hit;
             }
-            const bool has = kl && honest && (s_arr || ea || ra);
-            st_loads += (kl && real) ? 1u : 0u;
-            uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
-            bool es, rs, dl;
-            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
-            else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
-            else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
-            if (has) {   // lanes without arrivals keep their word: no store
-                const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
-                const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
-                (icells + (size_t)k * 64)[lane] = (uint64_t)nlo | ((uint64_t)nhi << 32);
+            const bool has = honest && (s_arr || ea || ra);
+            if (!__ballot(has)) return;                          // nothing lands on this key now
+            if (has) {
                 st_arr += ea + ra + (s_arr ? 1u : 0u);
                 st_cells += 1u;
             }
-            st_bcast += (es ? 1u : 0u) + (rs ? 1u : 0u);
+            // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
+            const bool opn = has && !(lo & F_DEL);
+            if (!__ballot(opn)) return;
+            uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
+            bool es = false, rs = false, dl = false;
+            const bool sa = opn && s_arr;
+            const uint32_t e = opn ? ea : 0u, r = opn ? ra : 0u;
+            if constexpr (BEB) {
+                brb_cell_update_beb(fl, sa, es, rs, dl);
+            } else if constexpr (SPEC) {
+                brb_cell_update_spec(fl, ec, rc, sa, e, r, T_echo, T_amp, T_del, es, rs, dl);
+            } else {
+                // brb_cell_update, its SEND / ECHO / READY stages run only when some message of
+                // that type lands (the skipped stages are identities)
+                if (s_win) {                                                     // :76-82
+                    es = sa && !(fl & F_EEX);
+                    fl |= es ? (F_EEX | F_ES) : 0u;
+                }
+                bool r1 = false, r2 = false;
+                if (be_any) {                                                    // :84-98
+                    const bool e_on = e != 0;
+                    const uint32_t checked = (fl & F_EEX) ? e : e - 1u;
+                    fl |= e_on ? F_EEX : 0u;
+                    ec += e;
+                    r1 = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX);
+                    fl |= r1 ? (F_REX | F_RS) : 0u;
+                }
+                if (br_any) {                                                    // :100-119
+                    const bool r_on = r != 0;
+                    const bool rex = (fl & F_REX) != 0;
+                    const uint32_t rlo = rex ? rc + 1u : 2u, rhi = rex ? rc + r : r;
+                    fl |= r_on ? F_REX : 0u;
+                    rc += r;
+                    const bool any = r_on && rhi >= rlo;
+                    const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+                    r2 = any && !(fl & F_EEX) && alo <= ahi && !(fl & F_RS);
+                    fl |= r2 ? F_RS : 0u;
+                    dl = any && rhi >= T_del;
+                    fl |= dl ? F_DEL : 0u;
+                }
+                rs = r1 || r2;
+            }
+            if (opn) {   // lanes whose cell is unchanged keep their word: no store
+                const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
+                const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
+                (icells + (size_t)k * 64)[lane] = (uint64_t)nlo | ((uint64_t)nhi << 32);
+                st_bcast += (es ? 1u : 0u) + (rs ? 1u : 0u);
+            }
             if (__ballot(dl)) {
                 if (dl) {
                     atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], 1ull << (k & 63));
@@ -814,7 +864,7 @@ void brc_step(const Params* pp) {
                     any_rows |= 1u << r;
                 }
                 const uint32_t myq = os ? t + hibit(os) : 0u;
-                if (kl && myq) {
+                if (myq) {
                     if (lane == 0 && myq > m_tquiet(m)) s_meta[k] = m_with_tquiet(m, myq);
                     q_until = max(q_until, myq);
                 }
@@ -1080,6 +1130,7 @@ void brc_step(const Params* pp) {
         }
     }
     st_msgs += st_bcast * n;
+    if (LEAN && real) st_loads += nk_lean;
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
 #pragma unroll

@@ -241,6 +241,9 @@ __device__ __forceinline__ uint64_t ring_put(uint64_t ring, uint32_t tl, uint32_
 // Every key-slot field is then wave-uniform, so the per-key work runs on scalar key ids,
 // metadata read once per chunk, exec-masked cell stores and (NLR = 2) link-delay masks held in
 // registers -- the headline configuration has exactly two link delays.
+#ifdef BRC_STAMPS
+__device__ unsigned long long brc_stamps[4];   // dev-only section timers (s_memtime ticks)
+#endif
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
 
 template <int NPAD, int DM, bool EV, int MODE, int NLR>
@@ -259,11 +262,14 @@ void brc_step(const Params* pp) {
     constexpr int IPW = 64 / NPAD;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
-    const int wid = threadIdx.x / 64, lane = threadIdx.x % 64;
+    // wid via readfirstlane: the item (and every address derived from it) is then provably wave-uniform
+    const int wid = (int)uni32(threadIdx.x / 64), lane = threadIdx.x % 64;
     const uint64_t item = (uint64_t)blockIdx.x * WPB + wid;
     if (item >= P.nitems) return;               // whole wave exits; waves never synchronise
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
+    // Q (phase window) and NV (key variants) are powers of two (brc_create): shifts, not divisions
+    const uint32_t qsh = (uint32_t)__ffs(Q) - 1u, Qm = Q - 1u, ksh = qsh + (uint32_t)__ffs(NV) - 1u;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
     //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16
     // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
@@ -450,7 +456,7 @@ void brc_step(const Params* pp) {
     // honest origin d broadcasts SEND for its key (d, s) with value v
     // (core/byzantinerandomizedconsensus.py:48-50 / :80-83 / :102-106, base/broadcast.py:30-35)
     auto send_key = [&](uint32_t s, uint32_t v) {
-        const uint32_t k = (d * NV) * Q + (s % Q);
+        const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint64_t m = s_meta[mbase + k];
         if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
         s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
@@ -473,7 +479,7 @@ void brc_step(const Params* pp) {
         for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
     };
     auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = (k / Q) / NV;
+        const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = k >> ksh;
         bool found = false;
         for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
         if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
@@ -504,7 +510,7 @@ void brc_step(const Params* pp) {
     // here), then the next round starts.
     auto spec_advance = [&]() {
         while (round > 0) {
-            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s % Q;
+            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s & Qm;
             const uint32_t cc = s_cnt[q * 64 + lane], n0 = (cc >> 10) & 0x3FF, n1 = cc >> 20;
             if ((seen_on ? popc(s_seen[q * 64 + lane]) : (cc & 0x3FF)) < n - P.f) return;
             if (seen_on) s_seen[q * 64 + lane] = 0;
@@ -534,11 +540,11 @@ void brc_step(const Params* pp) {
     };
     auto spec_deliver = [&](uint32_t k) {
         const uint64_t m = s_meta[mbase + k];
-        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = (k / Q) / NV;
+        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = k >> ksh;
         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
         if (s < cur) return;
         if (s >= cur + Q) { ovf = true; return; }
-        const uint32_t q = s % Q;
+        const uint32_t q = s & Qm;
         if (seen_on) {
             if ((s_seen[q * 64 + lane] >> host) & 1) return;
             s_seen[q * 64 + lane] |= (T)((T)1 << host);
@@ -604,7 +610,7 @@ void brc_step(const Params* pp) {
                                 gp(P.kdst)[inst * NK + k] = r.dst;
                                 mark_lane(k, os);
                                 st_msgs += __popcll(r.dst & all64);
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s, (uint32_t)(uint8_t)r.value);
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
                             }
                         }
                     }
@@ -635,7 +641,7 @@ void brc_step(const Params* pp) {
                             } else {
                                 sent = true;
                                 mycells[ri] = ring_put(ring, tl, t, c);
-                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
+                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                                 wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                                 mycells[(size_t)k * (CW * 64)] = wv;
                                 st_msgs += n;
@@ -646,7 +652,7 @@ void brc_step(const Params* pp) {
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                             mycells[(size_t)k * (CW * 64)] = wv;
                             st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
+                            log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                         }
                     }
                 }
@@ -677,6 +683,13 @@ void brc_step(const Params* pp) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
 
+#ifdef BRC_STAMPS
+    uint64_t stamp_acc[4] = {0, 0, 0, 0};
+    uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+#define BRC_STAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
+#else
+#define BRC_STAMP(i) do {} while (0)
+#endif
     for (uint32_t it = 0; it < P.max_steps; ++it) {
         const bool running0 = status == BRC_RUNNING;
         if (!__any(running0)) break;
@@ -707,6 +720,7 @@ void brc_step(const Params* pp) {
         }
         if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(0);
         // p < nkeys + CHUNK: padded list.  The key ids stay in SGPRs with the words they address,
         // so processing a key does not wait on another LDS round trip for its id.
         auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK], uint32_t (&kk)[CHUNK]) {
@@ -722,7 +736,7 @@ void brc_step(const Params* pp) {
         // (NLR), and only lanes whose cell changes store (exec-masked).
         const uint32_t tm0 = t - dly0, tm1 = t - dly1;
         const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
-        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd) {
+        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd, uint64_t& nw) {
             const uint32_t gen = gw & GEN_MASK;
             if (m_s1(m) == 0) return;                            // the slot holds no key
             ++nk_lean;                                           // lane loads: one word per real lane
@@ -827,10 +841,10 @@ void brc_step(const Params* pp) {
                 }
                 rs = r1 || r2;
             }
-            if (opn) {   // lanes whose cell is unchanged keep their word: no store
+            if (opn) {   // lanes whose cell is unchanged keep their word
                 const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
                 const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
-                (icells + (size_t)k * 64)[lane] = (uint64_t)nlo | ((uint64_t)nhi << 32);
+                nw = (uint64_t)nlo | ((uint64_t)nhi << 32);
                 st_bcast += (es ? 1u : 0u) + (rs ? 1u : 0u);
             }
             if (__ballot(dl)) {
@@ -840,7 +854,7 @@ void brc_step(const Params* pp) {
                 }
             }
             if (EV) {
-                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
                 if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
@@ -960,7 +974,7 @@ void brc_step(const Params* pp) {
             if (__ballot(dl))
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
             if (EV) {
-                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
                 if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
@@ -998,10 +1012,13 @@ void brc_step(const Params* pp) {
             auto cell = [&](uint32_t k) { return (icells + (size_t)k * 64)[lane]; };
             uint64_t w[CHUNK];
             uint32_t kk[CHUNK];
+            // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
+            // the compiler's wait for slot 0 would then drain every load)
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 kk[c] = kid(c);
                 w[c] = cell(kk[c]);
+                __builtin_amdgcn_sched_barrier(0);
             });
             for (uint32_t p = 0; p < nkeys; p += CHUNK) {
                 uint64_t mm[CHUNK];
@@ -1013,7 +1030,13 @@ void brc_step(const Params* pp) {
                 });
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c]);
+                    // exactly one whole-wave store per slot (unchanged lanes write their word back,
+                    // slots past the list write the trash row): with a fixed count of memory
+                    // operations between a load and its use, the compiler waits for exactly that
+                    // load (vmcnt(CHUNK - 1)) instead of for the younger stores as well
+                    uint64_t nw = w[c];
+                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c], nw);
+                    (icells + (size_t)kk[c] * 64)[lane] = nw;
                     kk[c] = kid(p + c + CHUNK);
                     w[c] = cell(kk[c]);
                 });
@@ -1038,6 +1061,7 @@ void brc_step(const Params* pp) {
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(1);
 
         // ================= consensus: this step's deliveries in canonical (kp, s) order
         {
@@ -1050,7 +1074,7 @@ void brc_step(const Params* pp) {
                 if (!cons) bits = 0;
                 while (bits) {
                     const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
-                    const uint32_t base = b0 - (b0 % Q);
+                    const uint32_t base = b0 & ~Qm;
                     uint64_t grp = bits & (gm0 << base);
                     bits &= ~(gm0 << base);
                     while (grp) {          // several phase indices of one origin: ascending s
@@ -1071,6 +1095,7 @@ void brc_step(const Params* pp) {
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(2);
 
         // ================= actions stamped t
         const bool inj_mine = do_actions();
@@ -1098,8 +1123,13 @@ void brc_step(const Params* pp) {
         if ((uint32_t)lane < nkw) s_act[row * nkw + lane] = 0;
         any_rows &= ~(1u << row);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(3);
     }
 
+#ifdef BRC_STAMPS
+    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+#endif
+#undef BRC_STAMP
     // ---- write back
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;

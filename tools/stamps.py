@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Dev-only: per-section cycle split of the lean step kernel on the cfg4 workload.
+Needs a variant built with -DBRC_STAMPS (tools/variant.py stamps -DBRC_STAMPS); run with
+BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances]."""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from byzantinerandomizedconsensus_amd import _lib as L  # noqa: E402
+from byzantinerandomizedconsensus_amd.engine import Engine  # noqa: E402
+
+inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+eng = Engine(n=64, f=21, instances=inst, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET,
+             delay_max=8, round_cap=1, step_cap=4000, key_window=4, variants=1, proposals=L.PROPOSALS_PHILOX)
+lib = ctypes.CDLL(os.environ["BRC_LIB"])
+out = (ctypes.c_ulonglong * 4)()
+eng.reset(); eng.run()
+lib.brc_dbg_stamps(out)
+eng.reset(); eng.run()
+lib.brc_dbg_stamps(out)
+tot = sum(out)
+names = ["step head + key list", "key loop (BRB cells)", "consensus deliveries", "actions + stop checks"]
+for nm, v in zip(names, out):
+    print("%-24s %6.1f %%  (%.3g ticks)" % (nm, 100.0 * v / tot, v))
+print("kernel ms %.2f" % eng.last_kernel_ms())

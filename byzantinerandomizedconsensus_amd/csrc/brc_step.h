@@ -480,8 +480,10 @@ void brc_step(const Params* pp) {
     };
     auto cons_deliver = [&](uint32_t k) {                            // :53-106
         const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = k >> ksh;
-        bool found = false;
-        for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
+        // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
+        const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
+        const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
+        const bool found = (~(x | (x >> 1)) & 0x55u & valid) != 0;
         if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
         s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
         ++vcount;                                                    // :61
@@ -734,7 +736,7 @@ void brc_step(const Params* pp) {
         // cell word.  Same transitions as process() below, with the per-key work cut down:
         // arrivals are matched against precomputed t - delay, the delay masks are registers
         // (NLR), and only lanes whose cell changes store (exec-masked).
-        const uint32_t tm0 = t - dly0, tm1 = t - dly1;
+        const uint32_t tm0 = t - dly0, tm1 = ndl > 1 ? t - dly1 : 0x10000u;   // 0x10000: no 16-bit step
         const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
         auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd, uint64_t& nw) {
             const uint32_t gen = gw & GEN_MASK;
@@ -750,16 +752,14 @@ void brc_step(const Params* pp) {
             uint32_t ea = 0, ra = 0;
             uint64_t be_any = 0, br_any = 0;
             if constexpr (NLR != 0) {
+                // for an honest receiver the delay classes partition the real senders (every link
+                // has one of the delays present: RL1 = real & ~RL0, and with one delay tm1 matches
+                // nothing), so each count is ONE popcount of a bitfield merge (v_bfi)
                 const uint64_t be0 = __ballot(tE == tm0), br0 = __ballot(tR == tm0);
-                if (be0) ea = popc(be0 & RL0);
-                if (br0) ra = popc(br0 & RL0);
-                be_any = be0; br_any = br0;
-                if (ndl > 1) {
-                    const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
-                    if (be1) ea += popc(be1 & RL1);
-                    if (br1) ra += popc(br1 & RL1);
-                    be_any |= be1; br_any |= br1;
-                }
+                const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
+                ea = popc((be0 & RL0) | (be1 & ~RL0));
+                ra = popc((br0 & RL0) | (br1 & ~RL0));
+                be_any = be0 | be1; br_any = br0 | br1;
             } else {
                 const uint32_t dE = t - tE, dR = t - tR;
                 Unrolled<DM>::run([&](auto jc) {

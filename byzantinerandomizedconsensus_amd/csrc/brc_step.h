@@ -248,7 +248,7 @@ template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 &
 
 template <int NPAD, int DM, bool EV, int MODE, int NLR>
 __global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? BRC_MIN_WAVES_LEAN : BRC_MIN_WAVES))
-void brc_step(const Params* pp) {
+void brc_step(const Params* __restrict__ pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
     // pinning ~60 of them in SGPRs across the hot loop.  Hot fields are copied to locals below.
@@ -1002,6 +1002,9 @@ void brc_step(const Params* pp) {
                 }
             }
         };
+        // lean key pipeline registers; declared here so they stay live to the end of the step (below)
+        uint64_t w[CHUNK];
+        uint32_t kk[CHUNK];
         if constexpr (LEAN) {
             // software pipeline, unrolled by CHUNK so the in-flight cell words never move between
             // registers: slot c holds key p + c; right after it is processed, slot c loads key
@@ -1010,8 +1013,6 @@ void brc_step(const Params* pp) {
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
             auto cell = [&](uint32_t k) { return (icells + (size_t)k * 64)[lane]; };
-            uint64_t w[CHUNK];
-            uint32_t kk[CHUNK];
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
             Unrolled<CHUNK>::run([&](auto ci) {
@@ -1122,6 +1123,13 @@ void brc_step(const Params* pp) {
         }
         if ((uint32_t)lane < nkw) s_act[row * nkw + lane] = 0;
         any_rows &= ~(1u << row);
+        if constexpr (LEAN) {
+            // The key loop's last refills load past the list (trash row) and nothing reads them;
+            // a use here keeps their registers from being reused by the consensus and action code
+            // above, which would otherwise wait for those loads right after the key loop.
+#pragma unroll
+            for (int c = 0; c < CHUNK; ++c) asm volatile("" ::"v"(w[c]));
+        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(3);
     }

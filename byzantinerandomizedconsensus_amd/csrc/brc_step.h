@@ -1073,25 +1073,23 @@ void brc_step(const Params* __restrict__ pp) {
                 uint64_t bits = s_dbits[w * 64 + lane];
                 s_dbits[w * 64 + lane] = 0;
                 if (!cons) bits = 0;
+                // one delivery per iteration, ascending slot = ascending (origin, variant); the slots
+                // of one key prefix hold its phase indices mod Q, so when several of them deliver in
+                // the same step (rare) the smallest phase index goes first
                 while (bits) {
-                    const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
-                    const uint32_t base = b0 & ~Qm;
-                    uint64_t grp = bits & (gm0 << base);
-                    bits &= ~(gm0 << base);
-                    while (grp) {          // several phase indices of one origin: ascending s
-                        uint32_t best = __ffsll((unsigned long long)grp) - 1;
-                        if (grp & (grp - 1)) {
-                            uint32_t bs = 0xFFFFFFFFu;
-                            for (uint64_t x = grp; x; x &= x - 1) {
-                                const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                                const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
-                                if (s1 < bs) { bs = s1; best = bb; }
-                            }
+                    uint32_t best = __ffsll((unsigned long long)bits) - 1;
+                    const uint64_t grp = bits & (gm0 << (best & ~Qm));
+                    if (grp & (grp - 1)) {
+                        uint32_t bs = 0xFFFFFFFFu;
+                        for (uint64_t x = grp; x; x &= x - 1) {
+                            const uint32_t bb = __ffsll((unsigned long long)x) - 1;
+                            const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
+                            if (s1 < bs) { bs = s1; best = bb; }
                         }
-                        grp &= ~(1ull << best);
-                        if constexpr (SPEC) spec_deliver(w * 64 + best);
-                        else cons_deliver(w * 64 + best);
                     }
+                    bits &= ~(1ull << best);
+                    if constexpr (SPEC) spec_deliver(w * 64 + best);
+                    else cons_deliver(w * 64 + best);
                 }
             }
         }

@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
 """Headline benchmark: decided consensus instances/sec at n=64, f=21 (BASELINE.json configs[3]).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--instances I]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--instances I] [--legs reference,spec]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (multi-GPU)
 
-Workload: 64 replicas, f = 21, the reference's protocol exactly as it
-runs (Bracha broadcast + two-phase consensus, reference quirks included), adversarial delays
-(messages from/to a per-instance slow set of f replicas take D = 8 steps, all others 1),
-Philox Bernoulli(1/2) proposals.  One "step" = one full pass of the hot path over the batch:
+Workload: 64 replicas, f = 21, adversarial delays (messages from/to a
+per-instance slow set of f replicas take D = 8 steps, all others 1), Philox Bernoulli(1/2)
+proposals, 2^20 instances per GPU.  One "step" = one full pass of the hot path over the batch:
 every instance simulated from its proposals until every honest replica has decided (the
 reference's decide() upcall, core/byzantinerandomizedconsensus.py:94).  Instances are
 independent, so ranks shard them (global Philox ids => results independent of N: weak
 scaling); the only collective is one RCCL all-reduce of the statistics.
 
-Prints ONE JSON line (rank 0).
+Two legs, one JSON line (rank 0):
+  reference  the protocol exactly as the reference runs it (quirks included) -- the headline
+             `value`.  Its coin branch is dead, so split proposals decide "-1" in
+             round 1; `decided_value_hist` shows that share.
+  spec       the protocol the reference intends, with the common coin made reachable (SURVEY §8
+             F3): "many coin rounds".  Its phase window Q = 8 doubles the cell footprint, so the
+             2^20 instances run as tiles of an engine re-keyed per tile (brc_reset_at): every timed
+             step covers all 2^20 instances; the statistics come from one extra untimed pass.
 """
 import argparse
 import json
@@ -26,7 +32,9 @@ sys.path.insert(0, ROOT)
 
 N_REPLICAS, F_FAULTS, DELAY_MAX, SEED, COIN_SEED = 64, 21, 8, 0x5EED0004, 0xC017C017
 SURVEY_BYTES_PER_CELL_STEP = 6 * ((N_REPLICAS + 7) // 8) + 2   # 50 B at n=64
+FLOOR_BYTES_PER_CELL_STEP = 16                                  # this layout: 8-B cell word read + written
 HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
+SPEC_TILE = 1 << 19                                             # SPEC (Q = 8) instances per engine tile
 
 
 def parse():
@@ -35,17 +43,19 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
-    ap.add_argument("--key-window", type=int, default=0, help="0: 4 (reference mode), 8 (spec mode)")
-    ap.add_argument("--mode", choices=("reference", "spec"), default="reference",
-                    help="reference: the protocol as the reference runs it (headline); spec: the intended "
-                         "protocol with its common coin (SURVEY §8 F3)")
+    ap.add_argument("--legs", default="reference,spec",
+                    help="comma list of reference (the headline value) and spec (SURVEY §8 F3 coin rounds)")
+    ap.add_argument("--mode", choices=("reference", "spec"), default=None,
+                    help="shorthand for --legs <mode> (the headline leg is the first one run)")
     ap.add_argument("--round-cap", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="collective backend for N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo "
                          "only rehearses the multi-rank flow with several ranks sharing one GPU")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.legs = [a.mode] if a.mode else [x for x in a.legs.split(",") if x]
+    return a
 
 
 def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
@@ -104,6 +114,120 @@ def load_traffic(instances, kernel_ms, mode="reference"):
     return d.get("hbm_bytes_per_launch")
 
 
+def make_engine(mode, count, first, device, round_cap):
+    from byzantinerandomizedconsensus_amd import _lib as L
+    from byzantinerandomizedconsensus_amd.engine import Engine
+    spec = mode == "spec"
+    return Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
+                  delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=round_cap, step_cap=4000,
+                  key_window=8 if spec else 4, variants=1, proposals=L.PROPOSALS_PHILOX,
+                  instance_offset=first, device=device, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
+                  coin_seed=COIN_SEED)
+
+
+def collect(eng):
+    """This engine's statistics, round histogram and decided values (one dict)."""
+    st = eng.stats()
+    hist = eng.round_histogram(66)
+    vals, dis = eng.decisions()
+    for k, v in vals.items():
+        st["dec_" + k] = v
+    st["disagreements"] = dis
+    return st, hist
+
+
+def add_stats(a, b):
+    if a is None:
+        return dict(b[0]), list(b[1])
+    st = {k: (max(a[0][k], v) if k == "max_t" else a[0].get(k, 0) + v) for k, v in b[0].items()}
+    return st, [x + y for x, y in zip(a[1], b[1])]
+
+
+def run_leg(args, mode, world, rank, local, dist, coll_dev):
+    """Time one leg (K steps after W warmups, barrier + sync on both sides, max over ranks)."""
+    from byzantinerandomizedconsensus_amd import shard
+    per = args.instances
+    first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
+    tile = count if mode == "reference" else min(count, SPEC_TILE)
+    tiles = [(first + o, min(tile, count - o)) for o in range(0, count, tile)]
+    eng = make_engine(mode, tiles[0][1], tiles[0][0], local, args.round_cap)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    def one_step():
+        kms = 0.0
+        for off, cnt in tiles:
+            if cnt != tiles[0][1]:
+                raise RuntimeError("uneven tiles: %d instances per GPU is not a multiple of %d" % (count, tile))
+            eng.reset_at(off)
+            eng.run()
+            kms += eng.last_kernel_ms()
+        return kms
+
+    for _ in range(args.warmup):
+        one_step()
+    barrier()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        kms.append(one_step())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(kms) / len(kms)          # all tiles of one step (= one launch per tile)
+    if len(tiles) == 1:
+        acc = collect(eng)                   # the last timed step's results
+    else:                                    # one more (untimed) pass reads every tile's results
+        acc = None
+        for off, cnt in tiles:
+            eng.reset_at(off)
+            eng.run()
+            acc = add_stats(acc, collect(eng))
+    eng.close()
+    st, hist = shard.reduce_stats(acc[0], dist, device=coll_dev, hist=acc[1])
+    elapsed = shard.max_over_ranks(elapsed, dist, device=coll_dev)
+    kernel_ms = shard.max_over_ranks(kernel_ms, dist, device=coll_dev)
+    decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
+    bad = st["overflow"] + st["stepcap"] + st["running"]
+    if bad:
+        print("WARNING: %s leg: %d instances did not finish cleanly" % (mode, bad), file=sys.stderr)
+    launches = len(tiles)
+    cs_gpu = cell_steps / world
+    achieved = SURVEY_BYTES_PER_CELL_STEP * cs_gpu / (kernel_ms / 1e3) / 1e9
+    floor = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / (kernel_ms / 1e3) / 1e9
+    traffic = load_traffic(per, kernel_ms, mode) if launches == 1 else None
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "traffic_frac": (traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "floor_frac": floor / HBM_PEAK_GBS,
+            "note": "algorithmic = %d B (SURVEY 8(d)) x %d cell-steps per GPU per step (%d launch%s): it credits "
+                    "n-bit ECHO/READY masks this design never moves (one 8-B word per cell), so frac can pass 1; "
+                    "the physical figures are floor_frac (%d B: the cell word read + written, per cell-step) and "
+                    "traffic_frac (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json)"
+                    % (SURVEY_BYTES_PER_CELL_STEP, cs_gpu, launches, "" if launches == 1 else "es",
+                       FLOOR_BYTES_PER_CELL_STEP)}
+    leg = {
+        "value": decided * args.steps / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "kernel_ms": kernel_ms,
+        "launches_per_step": launches,
+        "decided_fraction": decided / float(per * world),
+        "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
+        "decided_value_hist": {k: st["dec_" + k] for k in ("-1", "0", "1", "3", "undecided") if st["dec_" + k]},
+        "agreement_violations": st["disagreements"],
+        "replica_message_steps_per_s": arrivals * args.steps / elapsed,
+        "roofline": roof,
+        "workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
+                    % ("SPEC-protocol (common coin, phase window 8)" if mode == "spec" else "reference-protocol",
+                       "first decision" if args.round_cap == 1 else "%d decisions" % args.round_cap, per),
+    }
+    return leg
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,88 +248,38 @@ def main():
             tdist.init_process_group("gloo")
         dist = tdist
 
-    from byzantinerandomizedconsensus_amd import _lib as L
-    from byzantinerandomizedconsensus_amd import shard
-    from byzantinerandomizedconsensus_amd.engine import Engine
-
-    per = args.instances
-    spec = args.mode == "spec"
-    if not args.key_window:
-        args.key_window = 8 if spec else 4
-    first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
-    eng = Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
-                 delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=args.round_cap, step_cap=4000,
-                 key_window=args.key_window, variants=1, proposals=L.PROPOSALS_PHILOX,
-                 instance_offset=first, device=local, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
-                 coin_seed=COIN_SEED)
-
-    def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-
-    def one_step():
-        eng.reset()
-        eng.run()
-        return eng.last_kernel_ms()
-
-    for _ in range(args.warmup):
-        one_step()
-    barrier()
-    t0 = time.perf_counter()
-    kms = []
-    for _ in range(args.steps):
-        kms.append(one_step())
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = sum(kms) / len(kms)
-    # the only collective: statistics (RCCL over xGMI), max of the wall clocks
-    st, hist = shard.reduce_stats(eng.stats(), dist, device=coll_dev, hist=eng.round_histogram(66))
-    elapsed = shard.max_over_ranks(elapsed, dist, device=coll_dev)
-    kernel_ms = shard.max_over_ranks(kernel_ms, dist, device=coll_dev)
-    decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
-    bad = st["overflow"] + st["stepcap"] + st["running"]
-    if bad:
-        print("WARNING: %d instances did not finish cleanly" % bad, file=sys.stderr)
-    value = decided * args.steps / elapsed
+    legs = {mode: run_leg(args, mode, world, rank, local, dist, coll_dev) for mode in args.legs}
+    head_mode = args.legs[0]
+    head = legs[head_mode]
     out = None
     if rank == 0:
-        achieved = SURVEY_BYTES_PER_CELL_STEP * (cell_steps / world) / (kernel_ms / 1e3) / 1e9
-        traffic = load_traffic(per, kernel_ms, args.mode)
         out = {
             "metric": "decided consensus instances/sec (node) at n=64,f=21",
-            "value": value,
+            "value": head["value"],
             "unit": "instances/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
-            "config": {"workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
-                                   % ("SPEC-protocol (common coin)" if spec else "reference-protocol",
-                                      "first decision" if args.round_cap == 1 else "%d decisions" % args.round_cap,
-                                      per),
-                       "n": N_REPLICAS, "f": F_FAULTS, "instances_per_gpu": per, "round_cap": args.round_cap,
-                       "mode": args.mode, "key_window": args.key_window,
+            "config": {"workload": head["workload"], "n": N_REPLICAS, "f": F_FAULTS,
+                       "instances_per_gpu": args.instances, "round_cap": args.round_cap, "mode": head_mode,
+                       "key_window": 8 if head_mode == "spec" else 4,
                        "parallelism": "instance-sharded x%d" % world},
-            "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
-            "replica_message_steps_per_s": arrivals * args.steps / elapsed,
-            "decided_fraction": decided / float(per * world),
-            "kernel_ms": kernel_ms,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "note": "algorithmic = %d B (SURVEY 8(d)) x %d cell-steps per launch per GPU"
-                                 % (SURVEY_BYTES_PER_CELL_STEP, cell_steps // world)},
         }
-    eng.close()
+        for k in ("kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
+                  "agreement_violations", "replica_message_steps_per_s", "roofline"):
+            out[k] = head[k]
+        for mode, leg in legs.items():
+            if mode != head_mode:
+                out[mode + "_leg"] = leg
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:     # N = 1 only
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.mode, args.key_window, args.round_cap)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, head_mode, 8 if head_mode == "spec" else 4,
+                                           args.round_cap)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

@@ -97,6 +97,35 @@ __global__ void round_histogram(const uint64_t* cons1, const uint64_t* byz, uint
         if (sh[b]) atomicAdd(&hist[b], sh[b]);
 }
 
+// First decisions of the honest replicas (brc_read_decisions): per instance, count each honest
+// replica's first decided value id (bin 4: never decided) and flag instances whose honest replicas
+// decided different values.  One thread per instance; bins reduced in LDS first.
+__global__ void decision_histogram(const uint64_t* cons1, const uint64_t* byz, uint64_t instances, uint32_t ipw,
+                                   uint32_t lpi, uint32_t npad, uint32_t bw, uint32_t n,
+                                   unsigned long long* out /* [6]: 5 value bins, disagreements */) {
+    __shared__ unsigned long long sh[6];
+    if (threadIdx.x < 6) sh[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t in = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (in < instances) {
+        const uint64_t item = in / ipw, seg = in % ipw;
+        uint32_t cnt[5] = {0, 0, 0, 0, 0};
+        uint32_t seen = 0;                       // value ids decided by some honest replica
+        for (uint32_t d = 0; d < n; ++d) {
+            if ((byz[in * bw + d / 64] >> (d % 64)) & 1ull) continue;
+            const uint64_t c1 = cons1[item * lpi + seg * npad + d];
+            if ((c1 & 0xFFFF) == 0) { ++cnt[4]; continue; }
+            const uint32_t v = (uint32_t)(c1 >> 48) & 3u;      // first decided value id
+            ++cnt[v];
+            seen |= 1u << v;
+        }
+        for (int b = 0; b < 5; ++b) if (cnt[b]) atomicAdd(&sh[b], (unsigned long long)cnt[b]);
+        if (seen & (seen - 1)) atomicAdd(&sh[5], 1ull);
+    }
+    __syncthreads();
+    if (threadIdx.x < 6 && sh[threadIdx.x]) atomicAdd(&out[threadIdx.x], sh[threadIdx.x]);
+}
+
 // grid-stride fill: a dispatch holds < 2^32 work-items per dimension, and the cell array can
 // exceed that (2^17 instances x 512 key slots x 64 lanes = 2^32 words at n = 64, Q = 8)
 __global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
@@ -134,7 +163,9 @@ struct Engine {
     Params hparams;
     std::vector<std::vector<InjDev>> pending;   // per item: uploaded-but-unconsumed + new
     bool inj_dirty = false, pattern_active = false;
-    uint64_t gen_budget = 0;                     // generation advance bound since the last full clear
+    // slot generation budget: reallocations of one key slot are bounded by max phase index / Q + 2
+    // per epoch (brc_reset to brc_reset); gen_base sums the epochs since the last full clear
+    uint64_t gen_base = 0, gen_cur = 0;
     std::vector<std::pair<uint64_t, uint32_t>> send_keys;   // (instance, kp<<16|s) of injected SENDs
 };
 
@@ -196,7 +227,8 @@ static int clear_state(Engine* e, bool full) {
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipMemsetAsync(e->meta, 0, keys * 8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->mgen, 0, keys * 4, e->stream));
-        e->gen_budget = 0;
+        e->gen_base = 0;
+        e->gen_cur = 0;
     } else {
         hipLaunchKernelGGL(reset_slots, dim3((uint32_t)((keys + 255) / 256)), dim3(256), 0, e->stream, e->meta, e->mgen,
                            (uint64_t)keys);
@@ -491,6 +523,14 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
         e->err = "proposals not loaded";
         return BRC_E_STATE;
     }
+    // slot generations are 13-bit (wide kernel 11-bit) tags: past the budget a stale cell could
+    // read as current.  brc_reset clears fully once the budget is spent; a run that keeps stepping
+    // one simulation without resetting must stop here instead of risking the wrap.
+    const uint64_t gen_hard = (e->wide ? GEN_MASK_W : GEN_MASK) - 2;
+    if (e->gen_base + 2 >= gen_hard) {
+        e->err = "slot generation budget exhausted: call brc_reset";
+        return BRC_E_STATE;
+    }
     int rc = upload_injections(e);
     if (rc) return rc;
     Params P;
@@ -509,6 +549,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.nL = delay_values(c.delay_model, c.delay_max);
     P.event_cap = c.event_capacity;
     P.mode = c.mode; P.coin_seed = c.coin_seed;
+    // a slot allocated for phase index s has been reallocated at most gen_base + s/Q + 1 times
+    P.s_limit = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (gen_hard - 1 - e->gen_base) * c.key_window);
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
@@ -530,7 +572,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
     unsigned long long gc[8];
     HIPCHK(e, hipMemcpy(gc, e->gcount, sizeof(gc), hipMemcpyDeviceToHost));
-    e->gen_budget += gc[5] / c.key_window + 2;   // allocations of any one slot in this run
+    e->gen_cur = std::max<uint64_t>(e->gen_cur, gc[5] / c.key_window + 2);   // gc[5]: max phase index this epoch
     if (running_left) *running_left = (uint32_t)gc[6];   // counted by the step kernel
     return BRC_OK;
 }
@@ -539,7 +581,9 @@ int brc_reset(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return BRC_E_INVALID;
     HIPCHK(e, hipSetDevice(e->cfg.device));
-    int rc = clear_state(e, e->gen_budget >= (e->wide ? GEN_FULL_CLEAR_W : GEN_FULL_CLEAR));
+    const bool full = e->gen_base + e->gen_cur >= (e->wide ? GEN_FULL_CLEAR_W : GEN_FULL_CLEAR);
+    if (!full) { e->gen_base += e->gen_cur; e->gen_cur = 0; }
+    int rc = clear_state(e, full);   // full: gen_base = gen_cur = 0
     if (rc) return rc;
     for (auto& v : e->pending) v.clear();
     e->send_keys.clear();
@@ -688,6 +732,52 @@ int brc_read_round_histogram(void* h, uint64_t* hist, uint32_t bins) {
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
     (void)hipFree(dh);
     if (r != hipSuccess) { e->err = std::string("round histogram: ") + hipGetErrorString(r); return BRC_E_HIP; }
+    return BRC_OK;
+}
+
+int brc_read_decisions(void* h, uint64_t* value_hist, uint64_t* disagreements) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || !value_hist || !disagreements) return BRC_E_INVALID;
+    if (e->cfg.protocol != BRC_PROTO_CONSENSUS) { e->err = "decisions need the consensus protocol"; return BRC_E_STATE; }
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    unsigned long long* d = nullptr;
+    HIPCHK(e, hipMalloc(&d, 6 * 8));
+    hipError_t r = hipMemsetAsync(d, 0, 6 * 8, e->stream);
+    if (r == hipSuccess) {
+        const uint32_t tpb = 256;
+        const uint32_t blocks = (uint32_t)((e->cfg.instances + tpb - 1) / tpb);
+        hipLaunchKernelGGL(decision_histogram, dim3(blocks), dim3(tpb), 0, e->stream, e->cons1, e->byz,
+                           e->cfg.instances, (uint32_t)e->ipw, e->lpi, (uint32_t)e->npad, e->bw, e->cfg.n, d);
+        r = hipGetLastError();
+    }
+    unsigned long long hout[6] = {0};
+    if (r == hipSuccess) r = hipMemcpyAsync(hout, d, sizeof(hout), hipMemcpyDeviceToHost, e->stream);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (r != hipSuccess) { e->err = std::string("decision histogram: ") + hipGetErrorString(r); return BRC_E_HIP; }
+    for (int b = 0; b < 5; ++b) value_hist[b] = hout[b];
+    *disagreements = hout[5];
+    return BRC_OK;
+}
+
+int brc_reset_at(void* h, uint64_t instance_offset) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e) return BRC_E_INVALID;
+    e->cfg.instance_offset = instance_offset;
+    return brc_reset(h);
+}
+
+int brc_read_events_range(void* h, size_t first, brc_event* out, size_t cap, size_t* total) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || !total) return BRC_E_INVALID;
+    if (!e->event_count) { *total = 0; return BRC_OK; }
+    unsigned long long n = 0;
+    HIPCHK(e, hipMemcpy(&n, e->event_count, 8, hipMemcpyDeviceToHost));
+    *total = (size_t)n;
+    const size_t avail = std::min<size_t>((size_t)n, e->cfg.event_capacity);
+    if (out && cap && first < avail)
+        HIPCHK(e, hipMemcpy(out, e->events + first, std::min(avail - first, cap) * sizeof(brc_event),
+                            hipMemcpyDeviceToHost));
     return BRC_OK;
 }
 

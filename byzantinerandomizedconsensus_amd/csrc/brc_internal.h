@@ -58,7 +58,8 @@ struct Params {
     uint32_t T_echo, T_amp, T_del, T_cnt, bound_p1, bound_p2;
     uint64_t seed, inst_offset, instances, nitems;
     uint32_t max_steps, nL;   // nL: delay_values() of the run
-    uint32_t mode, pad0;      // BRC_MODE_*
+    uint32_t mode;            // BRC_MODE_*
+    uint32_t s_limit;         // phase indices >= s_limit overflow: the slot generation tags must not wrap
     uint64_t coin_seed;
     uint64_t event_cap;
     uint64_t* cells;

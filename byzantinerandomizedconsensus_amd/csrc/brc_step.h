@@ -458,7 +458,8 @@ void brc_step(const Params* __restrict__ pp) {
     auto send_key = [&](uint32_t s, uint32_t v) {
         const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint64_t m = s_meta[mbase + k];
-        if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
+        // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
+        if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
         s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
@@ -596,7 +597,7 @@ void brc_step(const Params* __restrict__ pp) {
                         uint64_t m = s_meta[mbase + k];
                         uint32_t gen = s_gen[mbase + k] & GEN_MASK;
                         const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
-                        if (!declared && m_s1(m) != 0 && t < m_tquiet(m)) {
+                        if ((!declared && m_s1(m) != 0 && t < m_tquiet(m)) || r.s >= P.s_limit) {
                             ovf = true;
                         } else {
                             uint32_t tq = m_tquiet(m);

@@ -281,7 +281,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     auto send_key = [&](uint32_t s, uint32_t v) {
         const uint32_t k = (d * NV) * Q + (s % Q);
         const uint64_t m = s_meta[k];
-        if (m_s1(m) != 0 && t < m_tquiet(m)) { ovf = true; return; }
+        // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
+        if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
         s_gen[k] = ((s_gen[k] & GEN_MASK_W) + 1) & GEN_MASK_W;
         s_meta[k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                         uint64_t m = s_meta[k];
                         uint32_t gen = s_gen[k] & GEN_MASK_W;
                         const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
-                        if (!declared && m_s1(m) != 0 && t < m_tquiet(m)) {
+                        if ((!declared && m_s1(m) != 0 && t < m_tquiet(m)) || r.s >= P.s_limit) {
                             ovf = true;
                         } else {
                             uint32_t tq = m_tquiet(m);

@@ -110,6 +110,12 @@ class Engine:
     def reset(self):
         self._chk(self._lib.brc_reset(self._h))
 
+    def reset_at(self, instance_offset):
+        """Reset and re-key the engine to global instances [instance_offset, +instances) (tiles a
+        range larger than one engine's footprint; results equal one engine over the range)."""
+        self._chk(self._lib.brc_reset_at(self._h, instance_offset))
+        self.cfg.instance_offset = instance_offset
+
     def last_kernel_ms(self):
         ms = ctypes.c_float(0)
         self._chk(self._lib.brc_last_kernel_ms(self._h, ctypes.byref(ms)))
@@ -145,6 +151,28 @@ class Engine:
             raise L.EngineError(L.E_STATE, "event log overflow: %d events, capacity %d"
                                 % (cnt.value, self.cfg.event_capacity))
         return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b, e.value) for e in arr[:cap]]
+
+    def events_since(self, first):
+        """Events first .. end of the log, and the new total: incremental draining (the log keeps
+        every event since the last reset)."""
+        total = ctypes.c_size_t(0)
+        self._chk(self._lib.brc_read_events_range(self._h, first, None, 0, ctypes.byref(total)))
+        if total.value > self.cfg.event_capacity:
+            raise L.EngineError(L.E_STATE, "event log overflow: %d events, capacity %d"
+                                % (total.value, self.cfg.event_capacity))
+        cap = total.value - first if total.value > first else 0
+        arr = (L.Event * max(1, cap))()
+        if cap:
+            self._chk(self._lib.brc_read_events_range(self._h, first, arr, cap, ctypes.byref(total)))
+        return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b, e.value) for e in arr[:cap]], total.value
+
+    def decisions(self):
+        """First decisions of the honest replicas: ({"-1": c, "0": c, "1": c, "3": c, "undecided": c},
+        instances whose honest replicas decided different values)."""
+        arr = np.zeros(5, dtype=np.uint64)
+        dis = ctypes.c_uint64(0)
+        self._chk(self._lib.brc_read_decisions(self._h, arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(dis)))
+        return dict(zip(("-1", "0", "1", "3", "undecided"), (int(x) for x in arr))), dis.value
 
     def round_histogram(self, bins=66):
         """hist[r] = instances whose honest replicas had all decided by round r; hist[0] =

@@ -251,8 +251,7 @@ class Cluster:
         return self.status
 
     def _dispatch(self):
-        evs = self.engine.events()
-        new, self.seen_events = evs[self.seen_events:], len(evs)
+        new, self.seen_events = self.engine.events_since(self.seen_events)   # only the new events
         by_t = {}
         for (_inst, t, kind, node, _typ, a, b, _v) in new:
             if kind in (L.EV_DELIVER, L.EV_DECIDE):

@@ -8,7 +8,9 @@ exchange.  The one collective is ``reduce_stats``: an all-reduce of the statisti
 """
 
 SUM_KEYS = ("instances", "running", "done", "quiescent", "stepcap", "overflow", "decided", "msgs_sent",
-            "arrivals", "cell_steps", "deliveries", "decide_rounds_sum", "events_dropped", "lane_loads")
+            "arrivals", "cell_steps", "deliveries", "decide_rounds_sum", "events_dropped", "lane_loads",
+            # Engine.decisions(): first decided value per honest replica, and disagreeing instances
+            "dec_-1", "dec_0", "dec_1", "dec_3", "dec_undecided", "disagreements")
 MAX_KEYS = ("max_t",)
 
 

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 2
+#define BRC_ABI_VERSION 3
 
 enum {
     BRC_OK = 0,
@@ -155,6 +155,20 @@ int brc_read_stats(void* engine, brc_stats* out);
  * undecided honest replica, rounds >= bins-1 in hist[bins-1].  bins in [2, 4096].  Per engine
  * (= per GPU shard); SURVEY §8(d) cfg5 all-reduces it over ranks (shard.reduce_stats). */
 int brc_read_round_histogram(void* engine, uint64_t* hist, uint32_t bins);
+/* Decisions of the honest replicas (consensus; the decide() upcall of
+ * core/byzantinerandomizedconsensus.py:94): value_hist[v] for v = 0..3 counts replicas whose FIRST
+ * decision carried value id v (0 is the reference's "-1"), value_hist[4] replicas that never
+ * decided; *disagreements counts instances whose honest replicas' first decisions differ
+ * (the agreement check of SURVEY §8(e)).  Per engine; shard.reduce_stats all-reduces them. */
+int brc_read_decisions(void* engine, uint64_t* value_hist /* [5] */, uint64_t* disagreements);
+/* brc_reset, then re-key the engine to the global instances [instance_offset, +instances): one
+ * engine sweeps a range larger than its device footprint in tiles, with the results one engine
+ * over the whole range would give (every Philox counter uses the global id).  Loaded proposals
+ * and Byzantine masks are kept (they are indexed by engine-local instance). */
+int brc_reset_at(void* engine, uint64_t instance_offset);
+/* Events first .. first+cap-1 of the log (brc_read_events reads from 0); *total = events logged
+ * since the last reset, dropped ones included.  Lets a caller drain the log incrementally. */
+int brc_read_events_range(void* engine, size_t first, brc_event* out, size_t cap, size_t* total);
 int brc_last_kernel_ms(void* engine, float* ms);
 int brc_device_count(int* count);
 const char* brc_last_error(void* engine);   /* engine NULL: why the last brc_create on this thread failed */

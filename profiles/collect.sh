@@ -1,14 +1,14 @@
 #!/bin/bash
 # rocprofv3 collection for the headline kernel (run on the GPU box from the repo root).
-#   bash profiles/collect.sh <tag> [instances]
+#   bash profiles/collect.sh <tag> [instances] [leg]     (leg: reference (default) or spec)
 # 1) kernel trace + stats of bench.py (same command the numbers come from)
 # 2) separate PMC passes (one counter block budget per pass, each under its own kill timeout)
 set -u
-TAG=${1:-r1}; INST=${2:-65536}
+TAG=${1:-r1}; INST=${2:-65536}; LEG=${3:-reference}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-BENCH="bench.py --instances $INST --steps 2 --warmup 1 --no-cpu"
+BENCH="bench.py --instances $INST --steps 2 --warmup 1 --no-cpu --legs $LEG"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- python3 $BENCH > $OUT/trace_bench.json 2> $OUT/trace.err || { echo "trace failed"; exit 1; }
 i=0
 for pmc in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_INSTS_SMEM GRBM_GUI_ACTIVE GRBM_COUNT"; do

@@ -69,8 +69,13 @@ def main():
         cfg = bench.get("config", {})
         out["instances"] = cfg.get("instances_per_gpu")
         out["workload"] = cfg.get("workload", "").split(":")[0]
+        out["mode"] = cfg.get("mode", "reference")
         out["bench_kernel_ms"] = bench.get("kernel_ms")
-    for path in (os.path.join(dest, "pmc_traffic.json"), os.path.join(os.path.dirname(dest.rstrip("/")), "pmc_traffic.json")):
+    # the bench reads profiles/pmc_traffic.json for its headline (reference) leg only
+    paths = [os.path.join(dest, "pmc_traffic.json")]
+    if out.get("mode", "reference") == "reference":
+        paths.append(os.path.join(os.path.dirname(dest.rstrip("/")), "pmc_traffic.json"))
+    for path in paths:
         with open(path, "w") as fh:
             json.dump(out, fh, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))

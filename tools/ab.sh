@@ -5,7 +5,7 @@
 # "tag kernel_ms value" lines and writes gpurun_out/ab/<tag>.<round>.json.
 set -u
 TAGS=$1; ROUNDS=$2; shift 2
-ARGS=${*:-"--instances 262144 --steps 3 --warmup 1 --no-cpu"}
+ARGS=${*:-"--instances 262144 --steps 3 --warmup 1 --no-cpu --legs reference"}
 mkdir -p gpurun_out/ab
 for r in $(seq 1 $ROUNDS); do
   for t in $TAGS; do

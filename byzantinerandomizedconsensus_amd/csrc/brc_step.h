@@ -796,63 +796,69 @@ void brc_step(const Params* __restrict__ pp) {
             }
             const bool has = honest && (s_arr || ea || ra);
             if (!__ballot(has)) return;                          // nothing lands on this key now
-            if (has) {
-                st_arr += ea + ra + (s_arr ? 1u : 0u);
-                st_cells += 1u;
-            }
+            // Per-lane work below is branch-free integer arithmetic on 0/1 flags: lane-mask logic
+            // and divergent branches would cost scalar (SALU) instructions, the busier issue port.
+            st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
+            st_cells += has ? 1u : 0u;
             // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
             const bool opn = has && !(lo & F_DEL);
             if (!__ballot(opn)) return;
             uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
-            bool es = false, rs = false, dl = false;
-            const bool sa = opn && s_arr;
+            uint32_t es = 0, rs = 0, dl = 0;                     // 0/1: ECHO sent, READY sent, delivered
+            const uint32_t sa = (opn && s_arr) ? 1u : 0u;
             const uint32_t e = opn ? ea : 0u, r = opn ? ra : 0u;
+            // 1 when a >= b (both < 2^31)
+            auto ge = [](uint32_t a, uint32_t b) -> uint32_t { return ((a - b) >> 31) ^ 1u; };
             if constexpr (BEB) {
-                brb_cell_update_beb(fl, sa, es, rs, dl);
+                bool bes, brs, bdl;
+                brb_cell_update_beb(fl, sa != 0, bes, brs, bdl);
+                dl = bdl ? 1u : 0u;
             } else if constexpr (SPEC) {
-                brb_cell_update_spec(fl, ec, rc, sa, e, r, T_echo, T_amp, T_del, es, rs, dl);
+                bool bes, brs, bdl;
+                brb_cell_update_spec(fl, ec, rc, sa != 0, e, r, T_echo, T_amp, T_del, bes, brs, bdl);
+                es = bes ? 1u : 0u; rs = brs ? 1u : 0u; dl = bdl ? 1u : 0u;
             } else {
-                // brb_cell_update, its SEND / ECHO / READY stages run only when some message of
-                // that type lands (the skipped stages are identities)
+                // brb_cell_update in integer form; its SEND / ECHO / READY stages run only when some
+                // message of that type lands (the skipped stages are identities).  F_EEX = bit 0,
+                // F_REX = 1, F_DEL = 2, F_ES = 3, F_RS = 4.
                 if (s_win) {                                                     // :76-82
-                    es = sa && !(fl & F_EEX);
-                    fl |= es ? (F_EEX | F_ES) : 0u;
+                    es = sa & ~fl & 1u;                                          // SEND, no ECHO entry
+                    fl |= es | (es << 3);                                        // F_EEX | F_ES
                 }
-                bool r1 = false, r2 = false;
                 if (be_any) {                                                    // :84-98
-                    const bool e_on = e != 0;
-                    const uint32_t checked = (fl & F_EEX) ? e : e - 1u;
-                    fl |= e_on ? F_EEX : 0u;
+                    const uint32_t eon = min(e, 1u);
+                    const uint32_t chk = min(e + (fl & 1u) - eon, 1u);           // a checked ECHO (:87-89)
+                    fl |= eon;                                                   // F_EEX
                     ec += e;
-                    r1 = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX);
-                    fl |= r1 ? (F_REX | F_RS) : 0u;
+                    const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;   // !F_REX (:95)
+                    fl |= (r1 << 1) | (r1 << 4);                                 // F_REX | F_RS
+                    rs = r1;
                 }
                 if (br_any) {                                                    // :100-119
-                    const bool r_on = r != 0;
-                    const bool rex = (fl & F_REX) != 0;
-                    const uint32_t rlo = rex ? rc + 1u : 2u, rhi = rex ? rc + r : r;
-                    fl |= r_on ? F_REX : 0u;
+                    const uint32_t ron = min(r, 1u);
+                    const uint32_t rex = (fl >> 1) & 1u;
+                    const uint32_t rexm = 0u - rex;                              // all ones iff F_REX
+                    const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = r + (rc & rexm);   // checked sizes
+                    fl |= ron << 1;                                              // F_REX
                     rc += r;
-                    const bool any = r_on && rhi >= rlo;
+                    const uint32_t any = ron & ge(rhi, rlo);
                     const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
-                    r2 = any && !(fl & F_EEX) && alo <= ahi && !(fl & F_RS);
-                    fl |= r2 ? F_RS : 0u;
-                    dl = any && rhi >= T_del;
-                    fl |= dl ? F_DEL : 0u;
+                    const uint32_t r2 = any & ~fl & ~(fl >> 4) & ge(ahi, alo) & 1u;     // !F_EEX, !F_RS
+                    fl |= r2 << 4;                                               // F_RS
+                    dl = any & ge(rhi, T_del);
+                    fl |= dl << 2;                                               // F_DEL
+                    rs |= r2;
                 }
-                rs = r1 || r2;
             }
-            if (opn) {   // lanes whose cell is unchanged keep their word
+            {   // new word for open cells; the others keep theirs
                 const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
                 const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
-                nw = (uint64_t)nlo | ((uint64_t)nhi << 32);
-                st_bcast += (es ? 1u : 0u) + (rs ? 1u : 0u);
+                nw = opn ? ((uint64_t)nlo | ((uint64_t)nhi << 32)) : nw;
+                st_bcast += es + rs;
             }
-            if (__ballot(dl)) {
-                if (dl) {
-                    atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], 1ull << (k & 63));
-                    st_del += 1u;
-                }
+            if (__ballot(dl != 0)) {
+                atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], (uint64_t)dl << (k & 63));
+                st_del += dl;
             }
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
@@ -880,7 +886,7 @@ void brc_step(const Params* __restrict__ pp) {
                 }
                 const uint32_t myq = os ? t + hibit(os) : 0u;
                 if (myq) {
-                    if (lane == 0 && myq > m_tquiet(m)) s_meta[k] = m_with_tquiet(m, myq);
+                    if (myq > m_tquiet(m)) s_meta[k] = m_with_tquiet(m, myq);   // uniform: every lane writes it
                     q_until = max(q_until, myq);
                 }
             }

@@ -739,7 +739,8 @@ void brc_step(const Params* __restrict__ pp) {
         // (NLR), and only lanes whose cell changes store (exec-masked).
         const uint32_t tm0 = t - dly0, tm1 = ndl > 1 ? t - dly1 : 0x10000u;   // 0x10000: no 16-bit step
         const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
-        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd, uint64_t& nw) {
+        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd, uint64_t& nw,
+                                bool& wr) {
             const uint32_t gen = gw & GEN_MASK;
             if (m_s1(m) == 0) return;                            // the slot holds no key
             ++nk_lean;                                           // lane loads: one word per real lane
@@ -853,7 +854,8 @@ void brc_step(const Params* __restrict__ pp) {
             {   // new word for open cells; the others keep theirs
                 const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
                 const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
-                nw = opn ? ((uint64_t)nlo | ((uint64_t)nhi << 32)) : nw;
+                nw = (uint64_t)nlo | ((uint64_t)nhi << 32);
+                wr = opn;
                 st_bcast += es + rs;
             }
             if (__ballot(dl != 0)) {
@@ -1043,8 +1045,13 @@ void brc_step(const Params* __restrict__ pp) {
                     // operations between a load and its use, the compiler waits for exactly that
                     // load (vmcnt(CHUNK - 1)) instead of for the younger stores as well
                     uint64_t nw = w[c];
-                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c], nw);
-                    (icells + (size_t)kk[c] * 64)[lane] = nw;
+                    bool wr = false;
+                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c], nw, wr);
+#ifdef BRC_WHOLE_STORE
+                    (icells + (size_t)kk[c] * 64)[lane] = wr ? nw : w[c];
+#else
+                    if (wr) (icells + (size_t)kk[c] * 64)[lane] = nw;
+#endif
                     kk[c] = kid(p + c + CHUNK);
                     w[c] = cell(kk[c]);
                 });

@@ -1038,6 +1038,10 @@ void brc_step(const Params* __restrict__ pp) {
                     mm[c] = s_meta[kk[c]];
                     gg[c] = s_gen[kk[c]];
                 });
+                // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
+                // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own
+                static_assert(CHUNK == 4, "four u16 key ids per 8-B read");
+                const uint64_t knext = *(const uint64_t*)&s_klist[p + CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     // exactly one whole-wave store per slot (unchanged lanes write their word back,
@@ -1052,7 +1056,7 @@ void brc_step(const Params* __restrict__ pp) {
 #else
                     if (wr) (icells + (size_t)kk[c] * 64)[lane] = nw;
 #endif
-                    kk[c] = kid(p + c + CHUNK);
+                    kk[c] = (uint32_t)(uni64(knext) >> (16 * c)) & 0xFFFFu;
                     w[c] = cell(kk[c]);
                 });
             }

@@ -220,6 +220,8 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
         "decided_value_hist": {k: st["dec_" + k] for k in ("-1", "0", "1", "3", "undecided") if st["dec_" + k]},
         "agreement_violations": st["disagreements"],
         "replica_message_steps_per_s": arrivals * args.steps / elapsed,
+        "counts": {k: st[k] for k in ("instances", "decided", "msgs_sent", "arrivals", "cell_steps", "deliveries",
+                                      "decide_rounds_sum", "lane_loads", "max_t")},
         "roofline": roof,
         "workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
                     % ("SPEC-protocol (common coin, phase window 8)" if mode == "spec" else "reference-protocol",
@@ -272,7 +274,7 @@ def main():
                        "parallelism": "instance-sharded x%d" % world},
         }
         for k in ("kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
-                  "agreement_violations", "replica_message_steps_per_s", "roofline"):
+                  "agreement_violations", "replica_message_steps_per_s", "counts", "roofline"):
             out[k] = head[k]
         for mode, leg in legs.items():
             if mode != head_mode:

@@ -7,8 +7,10 @@ unchanged on the MI355X engine.
 import importlib
 import sys
 
-_MODULES = ["base", "base.broadcast", "base.consensus", "core", "core.brbroadcast",
-            "core.byzantinerandomizedconsensus"]
+# network first: the core modules import it relatively (``from .. import network``), and every
+# alias must resolve to the one module object so all of them share one cluster registry
+_MODULES = ["network", "base", "base.broadcast", "base.consensus", "core", "core.brbroadcast",
+            "core.byzantinerandomizedconsensus", "core.bebroadcast"]
 
 for _m in _MODULES:
     sys.modules[__name__ + "." + _m] = importlib.import_module("byzantinerandomizedconsensus_amd." + _m)

@@ -43,6 +43,25 @@ def test_reference_import_paths():
             iface()
 
 
+def test_reference_path_bebroadcast_shares_the_cluster_registry():
+    # reference path core/bebroadcast.py:9; its relative `from .. import network` must land on the
+    # one network module, or a second cluster registry would split the peers
+    from byzantinerandomizedconsensus.core.bebroadcast import BEBroadcast
+    import byzantinerandomizedconsensus.network as alias_net
+    from byzantinerandomizedconsensus_amd.core import bebroadcast
+    assert BEBroadcast is bebroadcast.BEBroadcast
+    assert alias_net is network
+    peers = _peers(4, 6300)
+
+    class H:
+        def deliver(self, message):
+            pass
+
+    nodes = [BEBroadcast(p[1], peers, H()) for p in peers]
+    assert len({id(nd.cluster) for nd in nodes}) == 1
+    assert nodes[0].cluster is network.cluster_for(peers)
+
+
 def _peers(n, port=6000):
     return [("localhost", port + i) for i in range(n)]
 

@@ -1,0 +1,66 @@
+"""The engine's multi-rank path on the GPU: bench.py under torch.distributed.run, 2 ranks.
+
+Both ranks share GPU 0 and reduce over gloo (rehearsal backend: the RCCL all-reduce is the same
+`shard.reduce_stats` call with backend "nccl" on an 8-GPU node).  Each rank runs its contiguous
+shard of global instance ids through the HIP engine -- the code path the driver's multi-GPU bench
+takes -- and the all-reduced totals must equal ONE rank running every id: Philox draws use global
+ids, so the job's results do not depend on the rank count (weak scaling, no
+data-path exchange).  Both legs (reference protocol and SPEC coin rounds) are checked.
+
+torchrun and the single-rank bench are started as child processes before this process touches
+the GPU in this test; nothing replaces a GPU process image.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PER_RANK, WORLD = 4096, 2
+KEYS = ("decided_fraction", "decide_round_hist", "decided_value_hist", "agreement_violations", "counts")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _last_json(out):
+    for line in reversed(out.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            return json.loads(line)
+    raise AssertionError("no JSON line in bench output:\n" + out[-2000:])
+
+
+def _run(cmd, timeout):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, "rc %d\n%s\n%s" % (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
+    return _last_json(p.stdout)
+
+
+def _legs(d):
+    out = {"reference": {k: d[k] for k in KEYS}}
+    out["spec"] = {k: d["spec_leg"][k] for k in KEYS}
+    return out
+
+
+@pytest.mark.gpu
+def test_two_ranks_equal_one_rank_over_the_same_global_ids():
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec"]
+    multi = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(WORLD),
+                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                  "--gpus", str(WORLD), "--backend", "gloo", "--instances", str(PER_RANK)] + bench_args, 300)
+    single = _run([sys.executable, "bench.py", "--instances", str(PER_RANK * WORLD)] + bench_args, 300)
+    assert multi["n_gpus"] == WORLD and single["n_gpus"] == 1
+    assert multi["config"]["instances_per_gpu"] * WORLD == single["config"]["instances_per_gpu"]
+    m, s = _legs(multi), _legs(single)
+    for leg in ("reference", "spec"):
+        assert m[leg]["counts"]["instances"] == PER_RANK * WORLD
+        assert m[leg]["counts"]["decided"] > 0
+        assert m[leg] == s[leg], leg

@@ -550,7 +550,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.event_cap = c.event_capacity;
     P.mode = c.mode; P.coin_seed = c.coin_seed;
     // a slot allocated for phase index s has been reallocated at most gen_base + s/Q + 1 times
-    P.s_limit = (uint32_t)std::min<uint64_t>(0xFFFFFFFFull, (gen_hard - 1 - e->gen_base) * c.key_window);
+    // (and phase indices stay below 2^14 - 1: the narrow kernel's consensus snapshot keeps s + 1 in 14 bits)
+    P.s_limit = (uint32_t)std::min<uint64_t>(0x3FFEull, (gen_hard - 1 - e->gen_base) * c.key_window);
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;

@@ -33,6 +33,12 @@ constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before t
 constexpr uint32_t GEN_MASK_W = 0x7FF;      // wide kernel (n > 64): 11-bit cell generation
 constexpr uint32_t GEN_FULL_CLEAR_W = 1500;
 constexpr int CHUNK_W = 4;                  // wide kernel: keys whose ballots are exchanged per barrier
+#ifndef BRC_WIDE_DCW
+#define BRC_WIDE_DCW 4
+#endif
+constexpr uint32_t SQCAP = 4;               // wide kernel: SENDs one replica's consensus may start per step
+// wide kernel: delivery-bitmap words per receiver = key-list positions per pass / 64
+__host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw < BRC_WIDE_DCW ? nkw : BRC_WIDE_DCW; }
 constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
 #ifndef BRC_CHUNK
 #define BRC_CHUNK 4
@@ -87,20 +93,23 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
-// mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16 (tail padded with the trash row NK)
+// mgen[IPW*NK] u16 | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
+// reused as the consensus snapshot snap[IPW*NK] u16)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv, uint32_t rs) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
-    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 3) / 4 + (NK + 2 * CHUNK + 3) / 4);
+    // the key-list area doubles as the consensus phase's snapshot of every slot's (value, s + 1)
+    const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
+    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 3) / 4 + (klist_u16 + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
-// meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 | consensus area |
-// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 | klist[NK] u32 | red[12] u32 |
-// pmw[2][CHUNK_W][NW] u32
+// meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 | consensus area |
+// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | sq[SQCAP][NPAD] u32 | gen[NK] u16 | klist[NK] u16 |
+// red[12] u32 | pmw[2][CHUNK_W][NW] u32
 // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32 (one key variant per origin)
 __host__ __device__ inline uint32_t cons_words_wide(bool spec, uint32_t npad, uint32_t Q) {
     const uint32_t nw = npad / 64;
@@ -120,9 +129,9 @@ __host__ __device__ inline uint32_t xwords_wide(uint32_t model, uint32_t dmax, i
 
 __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec, uint32_t Q) {
     const uint32_t nw = (uint32_t)npad / 64;
-    return 8 * (NK + TS * nkw + nkw * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
+    return 8 * (NK + TS * nkw + dpos_words_wide(nkw) * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
                 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
-           4 * (NK + NK + 12 + 2 * CHUNK_W * nw);
+           4 * SQCAP * (uint32_t)npad + 2 * (NK + NK) + 4 * (12 + 2 * CHUNK_W * nw);
 }
 
 // Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of

@@ -4,6 +4,27 @@
 #include "brc_step.h"
 
 namespace brc {
+// Lean kernels with register-resident delay masks (NLR = 2): NPAD = 64, sender peers, at most two
+// distinct link delays (constant or slow-set models).
+static int launch_step_regmask(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s,
+                               const Params* P) {
+    if (mode == KMODE_CONN) return BRC_E_INVALID;
+#define BRC_CASE(DMX)                                                                                  \
+    if (dm == DMX) {                                                                                   \
+        if (mode == BRC_MODE_SPEC) return events ? launch_one<64, DMX, true, BRC_MODE_SPEC, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_SPEC, 2>(blocks, lds, s, P); \
+        if (mode == BRC_MODE_BEB) return events ? launch_one<64, DMX, true, BRC_MODE_BEB, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_BEB, 2>(blocks, lds, s, P); \
+        return events ? launch_one<64, DMX, true, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P); \
+    }
+#ifdef BRC_ONLY_DM8
+    BRC_CASE(8)
+#else
+    BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
+#endif
+#undef BRC_CASE
+    return BRC_E_INVALID;
+}
+
+
 int launch_step_64r(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
     return launch_step_regmask(dm, events, mode, blocks, lds, s, P);
 }

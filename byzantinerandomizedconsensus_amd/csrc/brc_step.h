@@ -287,6 +287,11 @@ void brc_step(const Params* __restrict__ pp) {
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
     uint16_t* s_gen = (uint16_t*)(s_dbits + 64 * nkw + h_words + l_words);   // gen | GEN16_RESTRICTED
     uint16_t* s_klist = s_gen + ((IPW * NK + 3) & ~3u);                      // this step's active key slots
+    // consensus phase: the key list is dead, and its area holds snap[IPW*NK] = value << 14 | (s + 1) of
+    // every slot as the BRB phase left it.  A replica's phase change reallocates its own slot
+    // mid-loop (send_key), while another replica may still have to count a delivery of the old key
+    // in that slot from this same step (its t_quiet may be this step): deliveries read the snapshot.
+    uint16_t* s_snap = s_klist;
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -480,7 +485,7 @@ void brc_step(const Params* __restrict__ pp) {
         for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
     };
     auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = m_value(s_meta[mbase + k]) & 3, host = k >> ksh;
+        const uint32_t v = (uint32_t)s_snap[mbase + k] >> 14, host = k >> ksh;   // snapshot (see s_snap)
         // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
         const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
         const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
@@ -542,8 +547,8 @@ void brc_step(const Params* __restrict__ pp) {
         }
     };
     auto spec_deliver = [&](uint32_t k) {
-        const uint64_t m = s_meta[mbase + k];
-        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = k >> ksh;
+        const uint32_t sn = s_snap[mbase + k];                      // snapshot (see s_snap)
+        const uint32_t s = (sn & 0x3FFFu) - 1u, v = sn >> 14, host = k >> ksh;
         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
         if (s < cur) return;
         if (s >= cur + Q) { ovf = true; return; }
@@ -1083,6 +1088,11 @@ void brc_step(const Params* __restrict__ pp) {
         BRC_STAMP(1);
 
         // ================= consensus: this step's deliveries in canonical (kp, s) order
+        for (uint32_t i = lane; i < IPW * NK; i += 64) {
+            const uint64_t m = s_meta[i];
+            s_snap[i] = (uint16_t)(((m_value(m) & 3u) << 14) | (m_s1(m) & 0x3FFFu));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         {
             const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
             const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
@@ -1101,7 +1111,7 @@ void brc_step(const Params* __restrict__ pp) {
                         uint32_t bs = 0xFFFFFFFFu;
                         for (uint64_t x = grp; x; x &= x - 1) {
                             const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                            const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
+                            const uint32_t s1 = s_snap[mbase + w * 64 + bb] & 0x3FFFu;
                             if (s1 < bs) { bs = s1; best = bb; }
                         }
                     }
@@ -1243,26 +1253,6 @@ int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hi
         if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \
         if (mode == BRC_MODE_BEB) return events ? launch_one<NPAD, DMX, true, BRC_MODE_BEB>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_BEB>(blocks, lds, s, P); \
         return events ? launch_one<NPAD, DMX, true, BRC_MODE_REFERENCE>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_REFERENCE>(blocks, lds, s, P); \
-    }
-#ifdef BRC_ONLY_DM8
-    BRC_CASE(8)
-#else
-    BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)
-#endif
-#undef BRC_CASE
-    return BRC_E_INVALID;
-}
-
-// Lean kernels with register-resident delay masks (NLR = 2): NPAD = 64, sender peers, at most two
-// distinct link delays (constant or slow-set models).
-inline int launch_step_regmask(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s,
-                               const Params* P) {
-    if (mode == KMODE_CONN) return BRC_E_INVALID;
-#define BRC_CASE(DMX)                                                                                  \
-    if (dm == DMX) {                                                                                   \
-        if (mode == BRC_MODE_SPEC) return events ? launch_one<64, DMX, true, BRC_MODE_SPEC, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_SPEC, 2>(blocks, lds, s, P); \
-        if (mode == BRC_MODE_BEB) return events ? launch_one<64, DMX, true, BRC_MODE_BEB, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_BEB, 2>(blocks, lds, s, P); \
-        return events ? launch_one<64, DMX, true, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P) : launch_one<64, DMX, false, BRC_MODE_REFERENCE, 2>(blocks, lds, s, P); \
     }
 #ifdef BRC_ONLY_DM8
     BRC_CASE(8)

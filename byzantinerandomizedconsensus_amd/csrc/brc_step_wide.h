@@ -42,7 +42,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 }
 
 template <int NPAD, int DM, bool EV, int MODE>
-__global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
+__global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
     // DM > 8 (geometric): in a given wave most delays carry no send, so each wave publishes which
@@ -58,27 +58,34 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     if (inst >= P.instances) return;            // whole workgroup exits
     const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, D = P.D, nkw = P.nkw, nL = P.nL;
     const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del, model = P.delay_model;
+    // Q and NV are powers of two (brc_create): shifts, not divisions
+    const uint32_t qsh = (uint32_t)__ffs(Q) - 1u, Qm = Q - 1u, ksh = qsh + (uint32_t)__ffs(NV) - 1u;
     // uniform / geometric delays: arrivals are matched on delay-code bit planes (xwords_wide), so
     // the exchange and the receiver's test cost the same however many delays are present
     const bool planes = plane_model(model);
     const uint32_t nX = planes ? (uint32_t)NPL + 1u : nL;   // exchanged words per (key, type)
-    // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dbits[nkw][NPAD] u64 |
-    //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | gen[NK] u32 |
-    //   klist[NK] u32 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
+    // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 |
+    //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | sq[SQCAP][NPAD] u32 |
+    //   gen[NK] u16 | klist[NK] u16 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
+    // dpos: this pass's deliveries, one bit per key-list POSITION (not per key slot): a step's keys
+    // are processed in passes of at most 64 DCW keys, which bounds the delivery bitmap (a slot-
+    // indexed one would take NK x NPAD bits and cap the CU at one workgroup)
     // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32
     uint64_t* s_meta = smem;
     uint64_t* s_act = s_meta + NK;
-    uint64_t* s_dbits = s_act + TS * nkw;
-    uint64_t* s_hm = s_dbits + (size_t)nkw * NPAD;
+    const uint32_t DCW = dpos_words_wide(nkw);     // delivery-bitmap words per receiver
+    uint64_t* s_dpos = s_act + TS * nkw;
+    uint64_t* s_hm = s_dpos + (size_t)DCW * NPAD;
     // SPEC, per phase slot q = s % Q: #origins | #"0" << 10 | #"1" << 20.  The wide engine takes
     // one key variant per origin (brc_create), so a replica delivers each (origin, phase) key at
     // most once and the origin count needs no host set.
     uint32_t* s_cnt = (uint32_t*)s_hm;
     uint64_t* s_xb = s_hm + cons_words_wide(SPEC, NPAD, Q);
     uint64_t* s_outm = s_xb + 2 * CHUNK_W * nX * 2 * NW;
-    uint32_t* s_gen = (uint32_t*)(s_outm + 16 * NW);
-    uint32_t* s_klist = s_gen + NK;
-    uint32_t* s_red = s_klist + NK;
+    uint32_t* s_sq = (uint32_t*)(s_outm + 16 * NW);    // deferred SENDs: (phase index << 8 | value)
+    uint16_t* s_gen = (uint16_t*)(s_sq + SQCAP * NPAD);  // 11-bit generations
+    uint16_t* s_klist = s_gen + NK;                    // key slots < 2^11
+    uint32_t* s_red = (uint32_t*)(s_klist + NK);       // NK is a multiple of 64: 4-B aligned
     uint32_t* s_pmw = s_red + 12;                // per wave: delays (compact index) with any send
     const uint32_t d = (uint32_t)tid;
     const uint64_t g = P.inst_offset + inst;
@@ -92,10 +99,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
     const uint32_t inj_off = gp(P.inj_off)[inst], inj_cnt = gp(P.inj_cnt)[inst];
     for (uint32_t i = d; i < NK; i += NPAD) {
         s_meta[i] = gp(P.meta)[inst * NK + i];
-        s_gen[i] = gp(P.mgen)[inst * NK + i];
+        s_gen[i] = (uint16_t)gp(P.mgen)[inst * NK + i];
     }
     for (uint32_t i = d; i < TS * nkw; i += NPAD) s_act[i] = gp(P.act)[inst * TS * nkw + i];
-    for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * NPAD + d] = 0;
+    for (uint32_t w = 0; w < DCW; ++w) s_dpos[w * NPAD + d] = 0;
     for (uint32_t i = d; i < 16 * NW; i += NPAD) s_outm[i] = 0;
     if (d < 12) s_red[d] = 0;
     uint32_t any_rows = uni32(gp(P.actany)[inst]);
@@ -279,17 +286,32 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         }
     };
     auto send_key = [&](uint32_t s, uint32_t v) {
-        const uint32_t k = (d * NV) * Q + (s % Q);
+        const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint64_t m = s_meta[k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
-        s_gen[k] = ((s_gen[k] & GEN_MASK_W) + 1) & GEN_MASK_W;
+        s_gen[k] = (uint16_t)(((s_gen[k] & GEN_MASK_W) + 1) & GEN_MASK_W);
         s_meta[k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
         st_msgs += n;
         st_smax = max(st_smax, s);
         log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s, v);
+    };
+    // Consensus runs between key-list passes, so the SENDs it starts are queued and performed after
+    // the step's last pass: every BRB message of the step (those of a key whose slot a new key
+    // reuses included) is processed before any slot is reallocated, as the serial semantics have it.
+    uint32_t nsq = 0;
+    auto send_later = [&](uint32_t s, uint32_t v) {
+        if (nsq < SQCAP) s_sq[nsq++ * NPAD + d] = (s << 8) | (v & 0xFF);
+        else ovf = true;                      // more phase transitions of one replica in one step
+    };
+    auto flush_sends = [&]() {
+        for (uint32_t i = 0; i < nsq; ++i) {
+            const uint32_t e = s_sq[i * NPAD + d];
+            send_key(e >> 8, e & 0xFF);
+        }
+        nsq = 0;
     };
     auto popc_hm = [&](uint32_t v) -> uint32_t {
         uint32_t c = 0;
@@ -309,16 +331,17 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             for (uint32_t w = 0; w < NW; ++w) hm(v, w) = 0;
     };
     auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = m_value(s_meta[k]) & 3, host = (k / Q) / NV;
-        bool found = false;
-        for (uint32_t i = 0; i < nvals; ++i) found |= ((order >> (2 * i)) & 3) == v;
+        const uint32_t v = m_value(s_meta[k]) & 3, host = k >> ksh;
+        // v already inserted? every 2-bit field of `order` compared at once (nvals <= 4)
+        const uint32_t x = order ^ (v * 0x55u);
+        const bool found = (~(x | (x >> 1)) & 0x55u & ((1u << (2 * nvals)) - 1u)) != 0;
         if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
         hm(v, host >> 6) |= 1ull << (host & 63);                     // :60
         ++vcount;                                                    // :61
         if (vcount >= P.T_cnt && phase == 1) {                       // :71
             const uint32_t prop = get_max_val(P.bound_p1);           // :73
             phase = 2; cons_reset();                                 // :75-78
-            send_key(2 * (round - 1) + 1, prop);                     // :80-83
+            send_later(2 * (round - 1) + 1, prop);                   // :80-83
         }
         if (vcount >= P.T_cnt && phase == 2) {                       // :86
             const uint32_t dec = get_max_val(P.bound_p2);            // :88
@@ -327,21 +350,21 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             lval = dec;
             log_ev(BRC_EV_DECIDE, d, 0, round, dec, dec);
             ++round; phase = 1; cons_reset();                        // :96-100
-            send_key(2 * (round - 1), dec);                          // :102-106
+            send_later(2 * (round - 1), dec);                        // :102-106
         }
     };
 
     // ---- SPEC consensus (as brc_step.h spec_advance / spec_deliver)
-    auto spec_advance = [&]() {
+    auto spec_advance = [&](bool defer) {
         while (round > 0) {
-            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s % Q;
+            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s & Qm;
             const uint32_t cc = cnt(q), n0 = (cc >> 10) & 0x3FF, n1 = cc >> 20;
             if ((cc & 0x3FF) < n - P.f) return;
             cnt(q) = 0;
             if (phase == 1) {
                 const uint32_t prop = (2 * n0 > n + P.f) ? 1u : (2 * n1 > n + P.f) ? 2u : 0u;
                 phase = 2;
-                send_key(s + 1, prop);
+                if (defer) send_later(s + 1, prop); else send_key(s + 1, prop);
             } else {
                 const uint32_t vmax = n1 > n0 ? 2u : 1u, cmax = max(n0, n1);
                 uint32_t est;
@@ -357,19 +380,18 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                     est = coin_id(P.coin_seed, g, round);
                 }
                 ++round; phase = 1;
-                send_key(s + 1, est);
+                if (defer) send_later(s + 1, est); else send_key(s + 1, est);
             }
         }
     };
     auto spec_deliver = [&](uint32_t k) {
         const uint64_t m = s_meta[k];
-        const uint32_t s = m_s1(m) - 1u, v = m_value(m), host = (k / Q) / NV;
+        const uint32_t s = m_s1(m) - 1u, v = m_value(m);
         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
         if (s < cur) return;
         if (s >= cur + Q) { ovf = true; return; }
-        (void)host;
-        cnt(s % Q) += 1u + (v == 1 ? 1u << 10 : 0u) + (v == 2 ? 1u << 20 : 0u);
-        spec_advance();
+        cnt(s & Qm) += 1u + (v == 1 ? 1u << 10 : 0u) + (v == 2 ? 1u << 20 : 0u);
+        spec_advance(true);
     };
 
     // ---- actions stamped t (performed after step t's messages); every branch is workgroup-uniform
@@ -382,7 +404,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                                                                          : (uint32_t)gp(P.prop)[inst * n + d];
                 round = 1; phase = 1;                                 // :43-47
                 send_key(0, v & 3);
-                if constexpr (SPEC) spec_advance();                   // phase 0 may be buffered
+                if constexpr (SPEC) spec_advance(false);              // phase 0 may be buffered
             }
         }
         while (inj_pos < inj_cnt) {
@@ -394,7 +416,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             if (r.kind == BRC_INJ_PROPOSE) {
                 if (mine && honest && d == r.node) {
                     round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
-                    if constexpr (SPEC) spec_advance();
+                    if constexpr (SPEC) spec_advance(false);
                 }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // every peer is a destination (brc_inject rejects restricted SENDs for n > 64)
@@ -416,12 +438,12 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[k] = m;
-                            s_gen[k] = gen;
+                            s_gen[k] = (uint16_t)gen;
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 mark_lane(k, os);
                                 st_msgs += n;
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, k / Q, r.s, (uint32_t)(uint8_t)r.value);
+                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
                             }
                         }
                     }
@@ -446,7 +468,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                             mycells[(size_t)k * NPAD] = wv;
                             st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, k / Q, r.s, m_value(m));
+                            log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                         }
                     }
                 }
@@ -485,7 +507,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
         t = next;
         const uint32_t row = t & (TS - 1);
 
-        // ================= BRB: this step's active key slots
+        // ================= BRB: this step's active key slots, as a key list in canonical (kp, s) order
         const uint32_t cells0 = st_cells;
         uint32_t nkeys = 0;
         for (uint32_t w = 0; w < nkw; ++w) {
@@ -493,11 +515,32 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             if (wid == 0) {
                 const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
-                if ((bits >> lane) & 1) s_klist[nkeys + below] = w * 64 + lane;
+                if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)(w * 64 + lane);
             }
             nkeys += (uint32_t)__popcll(bits);
         }
         __syncthreads();
+        {   // slot order is (kp, s mod Q): where one key prefix has several active slots (rare), order
+            // them by phase index so that list positions follow the canonical (kp, s) order
+            bool run = false;
+            for (uint32_t p = d; p + 1 < nkeys; p += NPAD) run |= (s_klist[p] >> qsh) == (s_klist[p + 1] >> qsh);
+            if (block_or(run ? 1u : 0u)) {
+                if (tid == 0) {
+                    for (uint32_t p = 1; p < nkeys; ++p) {          // insertion sort inside each prefix
+                        const uint16_t k = s_klist[p];
+                        const uint32_t s1 = m_s1(s_meta[k]);
+                        uint32_t q = p;
+                        while (q > 0 && (s_klist[q - 1] >> qsh) == (uint32_t)(k >> qsh) &&
+                               m_s1(s_meta[s_klist[q - 1]]) > s1) {
+                            s_klist[q] = s_klist[q - 1];
+                            --q;
+                        }
+                        s_klist[q] = k;
+                    }
+                }
+                __syncthreads();
+            }
+        }
 
         // phase 1 of a chunk: ballot words "my ECHO / READY of key c was sent dly steps ago"
         // The key id, meta word and generation it reads stay in SGPRs for phase 2 (process): meta
@@ -556,8 +599,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             });
         };
         // phase 2: one (receiver d, key k) cell
-        auto process = [&](const uint32_t k, const uint64_t wd, const uint64_t m, const uint32_t gw, uint32_t buf, int c)
-            __attribute__((always_inline)) {
+        auto process = [&](const uint32_t k, const uint64_t wd, const uint64_t m, const uint32_t gw, uint32_t buf, int c,
+                           uint32_t pos) __attribute__((always_inline)) {
             const uint32_t gen = gw & GEN_MASK_W;
             const bool kl = m_s1(m) != 0;                        // the slot holds a key
             const bool cur = kl && real && (((uint32_t)wd >> 21) & GEN_MASK_W) == gen;
@@ -638,9 +681,9 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
             st_cells += has ? 1u : 0u;
             st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
             st_del += dl ? 1u : 0u;
-            if (dl) s_dbits[(k >> 6) * NPAD + d] |= 1ull << (k & 63);
+            if (dl) s_dpos[(pos >> 6) * NPAD + d] |= 1ull << (pos & 63);   // pos: in this pass
             if (EV) {
-                const uint32_t kp = k / Q, s = m_s1(m) - 1u;
+                const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
                 if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
@@ -665,64 +708,56 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* pp) {
                 }
             }
         };
-        {
-            uint64_t wA[CHUNK_W];
-            uint32_t kA[CHUNK_W];
-            fetch(0, wA, kA);
-            for (uint32_t p = 0; p < nkeys; p += CHUNK_W) {
-                const uint32_t buf = (p / CHUNK_W) & 1;
-                uint64_t mA[CHUNK_W];
-                uint32_t gA[CHUNK_W];
-                ballots(p, buf, wA, kA, mA, gA);
-                __syncthreads();
-                uint64_t wB[CHUNK_W];
-                uint32_t kB[CHUNK_W];
-                fetch(p + CHUNK_W, wB, kB);
-                Unrolled<CHUNK_W>::run([&](auto ci) {
-                    constexpr int c = decltype(ci)::value;
-                    if (p + c < nkeys) process(kA[c], wA[c], mA[c], gA[c], buf, c);
-                });
-                Unrolled<CHUNK_W>::run([&](auto ci) {
-                    constexpr int c = decltype(ci)::value;
-                    wA[c] = wB[c];
-                    kA[c] = kB[c];
-                });
+        // passes of at most 64 DCW keys: BRB over the pass's keys, then the consensus over the pass's
+        // deliveries in list (= canonical) order; SENDs started by the consensus wait for the last pass
+        for (uint32_t base = 0; base < nkeys; base += 64 * DCW) {
+            const uint32_t end = min(nkeys, base + 64 * DCW);
+            {
+                uint64_t wA[CHUNK_W];
+                uint32_t kA[CHUNK_W];
+                fetch(base, wA, kA);
+                for (uint32_t p = base; p < end; p += CHUNK_W) {
+                    const uint32_t buf = (p / CHUNK_W) & 1;
+                    uint64_t mA[CHUNK_W];
+                    uint32_t gA[CHUNK_W];
+                    ballots(p, buf, wA, kA, mA, gA);
+                    __syncthreads();
+                    uint64_t wB[CHUNK_W];
+                    uint32_t kB[CHUNK_W];
+                    fetch(p + CHUNK_W, wB, kB);
+                    Unrolled<CHUNK_W>::run([&](auto ci) {
+                        constexpr int c = decltype(ci)::value;
+                        if (p + c < end) process(kA[c], wA[c], mA[c], gA[c], buf, c, p + c - base);
+                    });
+                    Unrolled<CHUNK_W>::run([&](auto ci) {
+                        constexpr int c = decltype(ci)::value;
+                        wA[c] = wB[c];
+                        kA[c] = kB[c];
+                    });
+                }
             }
-        }
-        __syncthreads();
-
-        // ================= consensus: this step's deliveries in canonical (kp, s) order
-        {
-            const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
-            const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest;
+            __syncthreads();
+            // ============= consensus: this pass's deliveries, ascending list position
+            {
+                const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest;
+                const uint32_t words = (end - base + 63) / 64;
 #pragma unroll 1
-            for (uint32_t w = 0; w < nkw; ++w) {
-                uint64_t bits = s_dbits[w * NPAD + d];
-                s_dbits[w * NPAD + d] = 0;
-                if (!cons) bits = 0;
-                while (bits) {
-                    const uint32_t b0 = __ffsll((unsigned long long)bits) - 1;
-                    const uint32_t base = b0 - (b0 % Q);
-                    uint64_t grp = bits & (gm0 << base);
-                    bits &= ~(gm0 << base);
-                    while (grp) {          // several phase indices of one origin: ascending s
-                        uint32_t best = __ffsll((unsigned long long)grp) - 1;
-                        if (grp & (grp - 1)) {
-                            uint32_t bs = 0xFFFFFFFFu;
-                            for (uint64_t x = grp; x; x &= x - 1) {
-                                const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                                const uint32_t s1 = m_s1(s_meta[w * 64 + bb]);
-                                if (s1 < bs) { bs = s1; best = bb; }
-                            }
-                        }
-                        grp &= ~(1ull << best);
-                        if constexpr (SPEC) spec_deliver(w * 64 + best);
-                        else cons_deliver(w * 64 + best);
+                for (uint32_t w = 0; w < words; ++w) {
+                    uint64_t bits = s_dpos[w * NPAD + d];
+                    s_dpos[w * NPAD + d] = 0;
+                    if (!cons) bits = 0;
+                    while (bits) {
+                        const uint32_t b = __ffsll((unsigned long long)bits) - 1;
+                        bits &= bits - 1;
+                        const uint32_t k = s_klist[base + w * 64 + b];
+                        if constexpr (SPEC) spec_deliver(k);
+                        else cons_deliver(k);
                     }
                 }
             }
+            __syncthreads();
         }
-        __syncthreads();
+        flush_sends();
 
         // ================= actions stamped t
         const bool inj_mine = do_actions();

@@ -46,8 +46,11 @@ class Codec:
     from ``payloads``, a {(kp, s): text} table, e.g. the strings given to ``broadcast``).
     """
 
-    def __init__(self, n, mode="consensus", nv=1, addrs=None, values=DEFAULT_VALUES, payloads=None):
-        self.n, self.mode, self.nv = n, mode, nv
+    def __init__(self, n, mode="consensus", nv=1, addrs=None, values=DEFAULT_VALUES, payloads=None,
+                 peer_mode="sender"):
+        if peer_mode not in ("sender", "connection"):
+            raise ValueError("peer_mode must be 'sender' or 'connection'")
+        self.n, self.mode, self.nv, self.peer_mode = n, mode, nv, peer_mode
         self.addrs = [tuple(a) for a in (addrs or default_addrs(n))]
         self.index = {a: i for i, a in enumerate(self.addrs)}
         self.values = list(values)
@@ -87,6 +90,12 @@ class Codec:
         dst_masks: {(t, node, type, kp, s): destination bit mask} for sends that did not go to
         every peer (the Byzantine injections that were restricted); everything else went to all.
         """
+        if self.peer_mode == "connection":
+            # connection-identity peers (core/brbroadcast.py:69): the :119 amplification re-sends
+            # READY once per qualifying READY, and the event log -- like the reference harness's
+            # send log -- records a broadcast only the first time, so the copies are not there
+            raise ValueError("wire export needs sender-identity peers: a connection-identity run re-sends "
+                             "READY copies that its event log records once")
         allm = (1 << self.n) - 1
         out = []
         for (inst, t, kind, node, typ, kp, s, value) in events:

@@ -8,7 +8,8 @@ cfg2: 10,000 instances n=4 f=1, honest, uniform delays [1,4] (one GPU).
 cfg3: one rank's shard of the 1M-instance n=16 f=5 run: 125,000 instances at global offset
       3 x 125,000, Byzantine {11..15} equivocating.
 cfg4: the bench batch, 131,072 instances n=64 f=21, slow-set delays D=8 (reference and SPEC).
-cfg5: n=256 f=85, 512 instances per delay model (SPEC).
+cfg4 at 2^20: the bench batch itself (reference protocol), 25 ids sampled across the range.
+cfg5: n=256 f=85, 512 instances per delay model (SPEC), 4 oracle-sampled ids per model.
 """
 import hashlib
 import random
@@ -136,23 +137,62 @@ def test_cfg4_bench_batch_full_size(mode):
         assert [r["first_decide_round"] for r in reps[j]] == [first[d] for d in range(64)]
 
 
+def _cfg5_cases():
+    import json
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cfg5_oracle.json")
+    with open(path) as fh:
+        return json.load(fh)["cases"]
+
+
 @pytest.mark.parametrize("model,dmax", [(0, 1), (1, 4), (3, 16)])
 def test_cfg5_n256_full_size(model, dmax):
+    """The 512-instance batch of each delay model; sampled ids equal the C oracle's results
+    (tests/golden/cfg5_oracle.json, made by tests/golden/make_cfg5_oracle.py: an n = 256 oracle
+    run takes about a minute) -- counters and every honest replica's first decision."""
     L = _L()
     N = 512
     kw = dict(n=256, f=85, protocol="consensus", seed=0x5EED0005, delay_model=model, delay_max=dmax,
               round_cap=1, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC,
               coin_seed=0xC017C017)
+    cases = [c for c in _cfg5_cases() if c["model"] == model and c["dmax"] == dmax]
+    assert cases
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
         res = eng.instances_result()
         hist = eng.round_histogram(66)
+        reps = {c["g"]: eng.replicas(c["g"], 1)[0] for c in cases}
     assert hist[0] == 0 and sum(hist) == N
     assert all(r["status"] == "done" for r in res)
-    if model != 0:
-        return
-    g = N - 1   # one instance vs the oracle (an n = 256 oracle run takes about a minute)
-    exp = oracle.run(S.spec_cons_spec(256, 85, 0x5EED0005, model, dmax, g, round_cap=1, window=8,
-                                      coin_seed=0xC017C017))
-    for k in KEYS:
-        assert res[g][k] == exp[k], (g, k)
+    for c in cases:
+        g = c["g"]
+        for k in KEYS:
+            assert res[g][k] == c[k], (model, g, k)
+        for d, (rep, exp) in enumerate(zip(reps[g], c["first_decide"])):
+            assert exp is not None, (g, d)
+            assert (rep["first_decide_round"], rep["first_decide_t"]) == (exp[0], exp[1]), (model, g, d)
+
+
+def test_cfg4_bench_batch_2p20_sampled():
+    """The bench's own batch (2^20 instances, reference protocol): instances sampled across the
+    whole id range equal the oracle run alone on their global id."""
+    L = _L()
+    N = 1 << 20
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=1, step_cap=4000, key_window=4, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_REFERENCE,
+              coin_seed=0xC017C017)
+    ids = sorted(random.Random(20).sample(range(N), 24)) + [N - 1]
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        hist = eng.round_histogram(66)
+        res = {i: eng.instances_result(i, 1)[0] for i in ids}
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    assert hist[0] == 0 and sum(hist) == N, "every instance decided"
+    for g in ids:
+        exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1))
+        for k in KEYS:
+            assert res[g][k] == exp[k], (g, k)
+        first = {}
+        for t, node, rnd, val in sorted(exp["events"]["decide"]):
+            first.setdefault(node, (rnd, t))
+        assert [(r["first_decide_round"], r["first_decide_t"]) for r in reps[g]] == [first[d] for d in range(64)], g

@@ -60,3 +60,14 @@ def test_byzantine_traffic_becomes_its_injections():
     norm = lambda xs: sorted(tuple(sorted((k, v) for k, v in x.items() if k != "value")) for x in xs)  # noqa: E731
     # declared keys carry no payload value in a BRB run; everything else must agree
     assert norm(got) == norm(want)
+
+
+def test_export_refuses_connection_identity_logs():
+    # a connection-identity run (core/brbroadcast.py:69) re-sends READY copies (:119) that the
+    # event log records once: exporting it as the complete wire would drop messages
+    from byzantinerandomizedconsensus_amd import wire
+    c = wire.Codec(4, peer_mode="connection")
+    with pytest.raises(ValueError):
+        c.export([(0, 1, wire.EV_SEND, 0, wire.SEND, 0, 0, 1)])
+    with pytest.raises(ValueError):
+        wire.Codec(4, peer_mode="tcp")

@@ -65,7 +65,11 @@ def main():
         if "SQ_INSTS_VMEM_RD" in k:
             out["vmem_rd_bytes_issued"] = k["SQ_INSTS_VMEM_RD"] * 512.0
             out["vmem_wr_bytes_issued"] = k.get("SQ_INSTS_VMEM_WR", 0.0) * 512.0
-    if bench:
+    if bench and "config" not in bench:             # a configs.py workload line
+        out["workload"], out["mode"] = bench.get("workload"), bench.get("mode")
+        out["instances"], out["bench_kernel_ms"] = bench.get("instances"), bench.get("kernel_ms")
+        out["headline"] = False
+    elif bench:
         cfg = bench.get("config", {})
         out["instances"] = cfg.get("instances_per_gpu")
         out["workload"] = cfg.get("workload", "").split(":")[0]
@@ -73,7 +77,7 @@ def main():
         out["bench_kernel_ms"] = bench.get("kernel_ms")
     # the bench reads profiles/pmc_traffic.json for its headline (reference) leg only
     paths = [os.path.join(dest, "pmc_traffic.json")]
-    if out.get("mode", "reference") == "reference":
+    if out.get("mode", "reference") == "reference" and out.get("headline", True):
         paths.append(os.path.join(os.path.dirname(dest.rstrip("/")), "pmc_traffic.json"))
     for path in paths:
         with open(path, "w") as fh:

@@ -326,7 +326,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const brc_config& c = *cfg;
     if (c.n < 1 || c.n > 256 || c.instances == 0 || c.delay_max < 1 || c.delay_max > 16 ||
         c.step_cap > STEP_LIMIT || c.peer_mode > BRC_PEER_CONNECTION ||
-        (c.peer_mode == BRC_PEER_CONNECTION && (c.mode != BRC_MODE_REFERENCE || c.n > 64 || c.delay_max > 8)) ||
+        (c.peer_mode == BRC_PEER_CONNECTION && c.mode != BRC_MODE_REFERENCE) ||
         (c.protocol != BRC_PROTO_BRB && c.protocol != BRC_PROTO_CONSENSUS) || c.delay_model > BRC_DELAY_GEOMETRIC ||
         (c.delay_model == BRC_DELAY_CONST && (c.delay_const < 1 || c.delay_const > c.delay_max)) ||
         !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8) ||
@@ -350,15 +350,19 @@ int brc_create(const brc_config* cfg, void** out) {
     e->bw = e->wide ? (uint32_t)e->npad / 64 : 1u;
     e->nkw_t = e->npad / 8 < 1 ? 1 : e->npad / 8;
     e->NK = (uint32_t)e->npad * c.variants * c.key_window;
-    // narrow kernel: + the trash row (brc_step.h); connection peers: 3 words per cell
-    e->rows = e->wide ? e->NK : (e->NK + 1) * (c.peer_mode == BRC_PEER_CONNECTION ? 3u : 1u);
+    // narrow kernel: + the trash row (brc_step.h); connection peers: 5 words per cell (the cell word
+    // and two 16-step send-count rings, brc_step.h Ring16)
+    const uint32_t cw = c.peer_mode == BRC_PEER_CONNECTION ? 5u : 1u;
+    e->rows = e->wide ? e->NK * cw : (e->NK + 1) * cw;
     e->nkw = (e->NK + 63) / 64;
     e->msize = e->npad <= 8 ? 1 : (uint32_t)e->npad / 8;
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
     e->regmask = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && nL <= 2;
-    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xwords_wide(c.delay_model, c.delay_max, e->dm),
+    // wide exchange words per (key, type): connection peers send 8 count planes per link delay
+    const uint32_t xw = c.peer_mode == BRC_PEER_CONNECTION ? 8u * nL : xwords_wide(c.delay_model, c.delay_max, e->dm);
+    e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xw,
                                             spec, c.key_window)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
                                                 c.variants, e->rs) * WPB;

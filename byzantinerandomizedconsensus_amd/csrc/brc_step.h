@@ -212,22 +212,29 @@ __device__ __forceinline__ void brb_cell_update_conn(uint32_t& fl, uint32_t& ec,
     n_ready = (r1 ? 1u : 0u) + fires;
 }
 
-// CONNECTION peers: a lane's send counts of one type over the last 8 steps, one byte per step
-// (slot = step mod 8); `tl` = the last step with a send (NEVER: none).  Valid because a send
-// reaches its receiver within D <= 8 steps and a cell is read before it is written in a step.
-__device__ __forceinline__ uint32_t ring_count(uint64_t ring, uint32_t tl, uint32_t s) {
-    return (tl != NEVER && s <= tl && tl - s < 8u) ? (uint32_t)(ring >> (8u * (s & 7u))) & 0xFFu : 0u;
+// CONNECTION peers: a lane's send counts of one type over the last 16 steps, one byte per step
+// (slot = step mod 16; slots 0-7 in `lo`, 8-15 in `hi`); `tl` = the last step with a send (NEVER:
+// none).  Valid because a send reaches its receiver within D <= 16 steps and a cell is read before
+// it is written in a step.  A count saturates nowhere below 255: one lane sends at most f + 1
+// READY copies of a key in one step (brb_cell_update_conn), and injections past 255 are refused.
+struct Ring16 { uint64_t lo, hi; };
+constexpr uint32_t RING_MAX = 255u;
+__device__ __forceinline__ uint32_t ring_count(const Ring16& r, uint32_t tl, uint32_t s) {
+    if (tl == NEVER || s > tl || tl - s >= 16u) return 0u;
+    return (uint32_t)(((s & 8u) ? r.hi : r.lo) >> (8u * (s & 7u))) & 0xFFu;
 }
-__device__ __forceinline__ uint64_t ring_put(uint64_t ring, uint32_t tl, uint32_t t, uint32_t c) {
-    if (tl == NEVER || t - tl >= 8u) {
-        ring = 0;
-    } else if (t != tl) {                        // clear the slots of steps tl+1 .. t
-        const uint32_t m = t - tl, r = 8u * ((tl + 1u) & 7u);
-        const uint64_t mask = (1ull << (8u * m)) - 1u;
-        ring &= ~(r ? ((mask << r) | (mask >> (64u - r))) : mask);
+__device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, uint32_t c) {
+    if (tl == NEVER || t - tl >= 16u) {
+        r.lo = r.hi = 0;
+    } else {
+        for (uint32_t s = tl + 1u; s != t + 1u; ++s) {  // clear the slots of steps tl+1 .. t
+            const uint64_t m = ~(0xFFull << (8u * (s & 7u)));
+            if (s & 8u) r.hi &= m; else r.lo &= m;
+        }
     }
-    const uint32_t sh = 8u * (t & 7u);
-    return (ring & ~(0xFFull << sh)) | ((uint64_t)min(c, 255u) << sh);
+    const uint64_t v = (uint64_t)min(c, RING_MAX) << (8u * (t & 7u)), m = ~(0xFFull << (8u * (t & 7u)));
+    if (t & 8u) r.hi = (r.hi & m) | v; else r.lo = (r.lo & m) | v;
+    return r;
 }
 
 #ifndef BRC_MIN_WAVES
@@ -256,7 +263,7 @@ void brc_step(const Params* __restrict__ pp) {
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     constexpr bool LEAN = lean_kernel<NPAD, MODE>();
     static_assert(NLR == 0 || (LEAN && NLR == 2), "register delay masks: lean kernels, two delays");
-    constexpr uint32_t CW = CONN ? 3 : 1;        // u64 words per cell (CONN: + ECHO and READY send rings)
+    constexpr uint32_t CW = CONN ? 5 : 1;        // u64 words per cell (CONN: + ECHO and READY send rings)
     using T = typename MaskOf<NPAD>::type;
     constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
     constexpr int IPW = 64 / NPAD;
@@ -411,7 +418,7 @@ void brc_step(const Params* __restrict__ pp) {
         if constexpr (NLR != 0) return j == 0 ? RL0 : RL1;
         else return s_L[j * 64 + lane];
     };
-    // cell (k, lane) at [k * CW * 64] (+ 64, + 128: CONN send rings)
+    // cell (k, lane) at [k * CW * 64] (CONN send rings: ECHO at + 64, + 128, READY at + 192, + 256)
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
@@ -640,15 +647,17 @@ void brc_step(const Params* __restrict__ pp) {
                         const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                         if constexpr (CONN) {
                             // every injected broadcast travels: one more send of this type at step t
-                            const size_t ri = (size_t)k * (CW * 64) + ((r.type == BRC_ECHO) ? 64 : 128);
+                            const size_t ri = (size_t)k * (CW * 64) + ((r.type == BRC_ECHO) ? 64 : 192);
                             const uint32_t tl = (uint32_t)(wv >> sh) & 0xFFFF;
-                            const uint64_t ring = mycells[ri];
+                            Ring16 ring = {mycells[ri], mycells[ri + 64]};
                             const uint32_t c = ring_count(ring, tl, t) + 1u;
-                            if (c > 31u) {
-                                badinj = true;                      // beyond the 5 count planes
+                            if (c > RING_MAX) {
+                                badinj = true;                      // beyond the one-byte count
                             } else {
                                 sent = true;
-                                mycells[ri] = ring_put(ring, tl, t, c);
+                                ring = ring_put(ring, tl, t, c);
+                                mycells[ri] = ring.lo;
+                                mycells[ri + 64] = ring.hi;
                                 if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                                 wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                                 mycells[(size_t)k * (CW * 64)] = wv;
@@ -913,10 +922,10 @@ void brc_step(const Params* __restrict__ pp) {
             const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
             const uint32_t dE = t - tE, dR = t - tR;             // steps since this lane sent
             uint32_t ea = 0, ra = 0;
-            uint64_t ringE = 0, ringR = 0;                       // CONN: this lane's send counts
+            Ring16 ringE = {0, 0}, ringR = {0, 0};               // CONN: this lane's send counts
             if constexpr (CONN) {
-                ringE = mycells[(size_t)k * (CW * 64) + 64];
-                ringR = mycells[(size_t)k * (CW * 64) + 128];
+                ringE = {mycells[(size_t)k * (CW * 64) + 64], mycells[(size_t)k * (CW * 64) + 128]};
+                ringR = {mycells[(size_t)k * (CW * 64) + 192], mycells[(size_t)k * (CW * 64) + 256]};
                 uint32_t j = 0;
                 for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
                     const uint32_t dly = (uint32_t)__ffs(ds);
@@ -924,7 +933,7 @@ void brc_step(const Params* __restrict__ pp) {
                     if (__ballot((ce | cr) != 0)) {               // arrivals = sum over senders of counts:
                         const T Lj = s_L[j * 64 + lane];         // one ballot per count bit
 #pragma unroll
-                        for (int b = 0; b < 5; ++b) {
+                        for (int b = 0; b < 8; ++b) {
                             const uint64_t be = __ballot((ce >> b) & 1u), br = __ballot((cr >> b) & 1u);
                             ea += popc((T)(be >> segbase) & Lj) << b;
                             ra += popc((T)(br >> segbase) & Lj) << b;
@@ -970,8 +979,14 @@ void brc_step(const Params* __restrict__ pp) {
                 ec = min(ec, 127u); rc = min(rc, 127u);
                 if (es) ringE = ring_put(ringE, tE, t, 1u);
                 if (rs) ringR = ring_put(ringR, tR, t, n_ready);
-                mycells[(size_t)k * (CW * 64) + 64] = ringE;
-                mycells[(size_t)k * (CW * 64) + 128] = ringR;
+                if (es) {
+                    mycells[(size_t)k * (CW * 64) + 64] = ringE.lo;
+                    mycells[(size_t)k * (CW * 64) + 128] = ringE.hi;
+                }
+                if (rs) {
+                    mycells[(size_t)k * (CW * 64) + 192] = ringR.lo;
+                    mycells[(size_t)k * (CW * 64) + 256] = ringR.hi;
+                }
             } else if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
             else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
@@ -1242,12 +1257,13 @@ int launch_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
 
 template <int NPAD>
 int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    if (mode == KMODE_CONN && dm > 8) return BRC_E_INVALID;
-    // connection-identity peers: reference protocol, D <= 8 (brc_create)
+    // connection-identity peers: reference protocol, D <= 16 (brc_create)
     if (mode == KMODE_CONN && dm == 4) return events ? launch_one<NPAD, 4, true, KMODE_CONN>(blocks, lds, s, P)
                                                      : launch_one<NPAD, 4, false, KMODE_CONN>(blocks, lds, s, P);
     if (mode == KMODE_CONN && dm == 8) return events ? launch_one<NPAD, 8, true, KMODE_CONN>(blocks, lds, s, P)
                                                      : launch_one<NPAD, 8, false, KMODE_CONN>(blocks, lds, s, P);
+    if (mode == KMODE_CONN && dm == 16) return events ? launch_one<NPAD, 16, true, KMODE_CONN>(blocks, lds, s, P)
+                                                      : launch_one<NPAD, 16, false, KMODE_CONN>(blocks, lds, s, P);
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
         if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \

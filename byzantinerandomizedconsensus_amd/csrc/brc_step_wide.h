@@ -44,7 +44,9 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 template <int NPAD, int DM, bool EV, int MODE>
 __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
-    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB;
+    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
+    // u64 words per cell: CONN adds the lane's ECHO and READY send-count rings (Ring16, brc_step.h)
+    constexpr uint32_t CW = CONN ? 5 : 1;
     // DM > 8 (geometric): in a given wave most delays carry no send, so each wave publishes which
     // did (pmw) and the readers visit only those; with DM <= 8 that bookkeeping costs more than it
     // saves (measured cfg5: geometric -20% kernel time, const/uniform +5%)
@@ -62,8 +64,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     const uint32_t qsh = (uint32_t)__ffs(Q) - 1u, Qm = Q - 1u, ksh = qsh + (uint32_t)__ffs(NV) - 1u;
     // uniform / geometric delays: arrivals are matched on delay-code bit planes (xwords_wide), so
     // the exchange and the receiver's test cost the same however many delays are present
-    const bool planes = plane_model(model);
-    const uint32_t nX = planes ? (uint32_t)NPL + 1u : nL;   // exchanged words per (key, type)
+    // CONN: a sender's copies of one type may span several send steps, so the exchange is per link
+    // delay (compact index j) and carries the copy count as 8 bit planes (8 nL words, brc_create)
+    const bool planes = !CONN && plane_model(model);
+    const uint32_t nX = CONN ? 8u * nL : planes ? (uint32_t)NPL + 1u : nL;   // exchanged words per (key, type)
     // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 |
     //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | sq[SQCAP][NPAD] u32 |
     //   gen[NK] u16 | klist[NK] u16 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
@@ -220,7 +224,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     dlist = uni64(dlist);
     const uint32_t maxout = hibit(outset);
     bool ovf = (uint32_t)__popc(dset) > nL, badinj = false;   // cannot happen: delay_values() bounds dset
-    const gptr_t<uint64_t> mycells = gp(P.cells) + inst * (uint64_t)NK * NPAD + d;   // cell (k, d) at [k * NPAD]
+    // cell (k, d) at [k * CW * NPAD]; CONN rings: ECHO at + NPAD, + 2 NPAD, READY at + 3 NPAD, + 4 NPAD
+    const gptr_t<uint64_t> mycells = gp(P.cells) + inst * (uint64_t)NK * CW * NPAD + d;
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
@@ -458,15 +463,33 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                         badinj = true;
                     } else {
                         const uint32_t gen = s_gen[k] & GEN_MASK_W;
-                        uint64_t wv = mycells[(size_t)k * NPAD];
+                        uint64_t wv = mycells[(size_t)k * (CW * NPAD)];
                         if (((wv >> 21) & GEN_MASK_W) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 21);
                         const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
-                        if (!(wv & bit)) {
+                        const int sh = (r.type == BRC_ECHO) ? 32 : 48;
+                        if constexpr (CONN) {
+                            // every injected broadcast travels: one more send of this type at step t
+                            const gptr_t<uint64_t> rp = mycells + (size_t)k * (CW * NPAD) + ((r.type == BRC_ECHO) ? NPAD : 3 * NPAD);
+                            const uint32_t tl = (uint32_t)(wv >> sh) & 0xFFFF;
+                            Ring16 ring = {rp[0], rp[NPAD]};
+                            const uint32_t c = ring_count(ring, tl, t) + 1u;
+                            if (c > RING_MAX) {
+                                badinj = true;                      // beyond the one-byte count
+                            } else {
+                                sent = true;
+                                ring = ring_put(ring, tl, t, c);
+                                rp[0] = ring.lo;
+                                rp[NPAD] = ring.hi;
+                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                                wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                                mycells[(size_t)k * (CW * NPAD)] = wv;
+                                st_msgs += n;
+                            }
+                        } else if (!(wv & bit)) {
                             sent = true;
                             wv |= bit;
-                            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                             wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            mycells[(size_t)k * NPAD] = wv;
+                            mycells[(size_t)k * (CW * NPAD)] = wv;
                             st_msgs += n;
                             log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                         }
@@ -559,6 +582,27 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
                     uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nX) * 2 * NW;
+                    if constexpr (CONN) {
+                        // per delay present: the 8 bit planes of "copies I sent dly steps ago"
+                        const gptr_t<uint64_t> rp = mycells + (size_t)k * (CW * NPAD);
+                        const Ring16 rE = {rp[NPAD], rp[2 * NPAD]}, rR = {rp[3 * NPAD], rp[4 * NPAD]};
+                        const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
+                        uint32_t j = 0, pm = 0;
+                        for (uint32_t ds = dset; ds; ds &= ds - 1, ++j) {
+                            const uint32_t dly = (uint32_t)__ffs(ds);
+                            const uint32_t ce = ring_count(rE, tE, t - dly), cr = ring_count(rR, tR, t - dly);
+                            if (__ballot((ce | cr) != 0)) {
+                                pm |= 1u << j;
+#pragma unroll
+                                for (int b = 0; b < 8; ++b) {
+                                    const uint64_t be = __ballot((ce >> b) & 1u), br = __ballot((cr >> b) & 1u);
+                                    if (lane == 0) { xb[(j * 8 + b) * 2 * NW + wid] = be; xb[(j * 8 + b) * 2 * NW + NW + wid] = br; }
+                                }
+                            }
+                        }
+                        if (lane == 0) s_pmw[(buf * CHUNK_W + c) * NW + wid] = pm;
+                        return;
+                    }
                     if (planes) {
                         // code = steps since this lane sent - 1; a receiver matches it against the
                         // code of its link from this lane, plane by plane
@@ -594,7 +638,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                 kk[c] = 0;
                 if (p + c < nkeys) {
                     kk[c] = uni32(s_klist[p + c]);
-                    ww[c] = mycells[(size_t)kk[c] * NPAD];
+                    ww[c] = mycells[(size_t)kk[c] * (CW * NPAD)];
                 }
             });
         };
@@ -611,7 +655,26 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                 // only the delays at which some wave had a send (each wave's pmw word); a wave that
                 // had none there did not write its ballot words, so they read as zero
                 const uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nX) * 2 * NW;
-                if (planes) {
+                if constexpr (CONN) {
+                    // arrivals = sum over senders of their copy counts (one popcount per bit plane)
+                    uint32_t pwv[NW], pm = 0;
+#pragma unroll
+                    for (int w = 0; w < NW; ++w) { pwv[w] = uni32(s_pmw[(buf * CHUNK_W + c) * NW + w]); pm |= pwv[w]; }
+                    for (; pm; pm &= pm - 1) {
+                        const uint32_t j = (uint32_t)__ffs(pm) - 1, dly = (uint32_t)((dlist >> (4 * j)) & 15u) + 1u;
+                        Unrolled<NW>::run([&](auto wc) {
+                            constexpr int w = decltype(wc)::value;
+                            if ((pwv[w] >> j) & 1u) {
+                                const uint64_t L = Lw(dly, wc);
+#pragma unroll
+                                for (int b = 0; b < 8; ++b) {
+                                    ea += (uint32_t)__popcll(xb[(j * 8 + b) * 2 * NW + w] & L) << b;
+                                    ra += (uint32_t)__popcll(xb[(j * 8 + b) * 2 * NW + NW + w] & L) << b;
+                                }
+                            }
+                        });
+                    }
+                } else if (planes) {
                     // senders whose send is `code + 1` steps old, where code is their link's delay
                     // code to this receiver: no plane differs (PL = 0 off the real receivers,
                     // whose counts are never used)
@@ -668,24 +731,40 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             st_loads += (kl && real) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 255, rc = (uint32_t)(word >> 13) & 255;
             bool es, rs, dl;
-            if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
+            uint32_t n_ready = 0;                                // CONN: READY broadcasts this step
+            bool first_ready = false;
+            if constexpr (CONN) {
+                brb_cell_update_conn(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, n_ready, dl);
+                rs = n_ready != 0;
+                first_ready = rs && !(fl & F_RS);
+                fl |= rs ? F_RS : 0u;
+                const gptr_t<uint64_t> rp = mycells + (size_t)k * (CW * NPAD);
+                if (es) {
+                    const Ring16 r = ring_put(Ring16{rp[NPAD], rp[2 * NPAD]}, tE, t, 1u);
+                    rp[NPAD] = r.lo; rp[2 * NPAD] = r.hi;
+                }
+                if (rs) {
+                    const Ring16 r = ring_put(Ring16{rp[3 * NPAD], rp[4 * NPAD]}, tR, t, n_ready);
+                    rp[3 * NPAD] = r.lo; rp[4 * NPAD] = r.hi;
+                }
+            } else if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
             else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             {
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)min(ec, 255u) << 5) | ((uint64_t)min(rc, 255u) << 13) |
                                     ((uint64_t)gen << 21) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
-                mycells[(size_t)k * NPAD] = has ? nw : wd;
+                mycells[(size_t)k * (CW * NPAD)] = has ? nw : wd;
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;
-            st_msgs += ((es ? 1u : 0u) + (rs ? 1u : 0u)) * n;
+            st_msgs += ((es ? 1u : 0u) + (CONN ? n_ready : (rs ? 1u : 0u))) * n;
             st_del += dl ? 1u : 0u;
             if (dl) s_dpos[(pos >> 6) * NPAD + d] |= 1ull << (pos & 63);   // pos: in this pass
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
                 if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
-                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
@@ -839,6 +918,7 @@ int launch_step_wide(int dm, bool events, int mode, uint32_t blocks, uint32_t ld
     if (dm == DMX) {                                                                                   \
         if (mode == BRC_MODE_SPEC) return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \
         if (mode == BRC_MODE_BEB) return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_BEB>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_BEB>(blocks, lds, s, P); \
+        if (mode == KMODE_CONN) return events ? launch_wide_one<NPAD, DMX, true, KMODE_CONN>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, KMODE_CONN>(blocks, lds, s, P); \
         return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_REFERENCE>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_REFERENCE>(blocks, lds, s, P); \
     }
     BRC_CASE(4) BRC_CASE(8) BRC_CASE(16)

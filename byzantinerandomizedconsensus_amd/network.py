@@ -26,6 +26,10 @@ Deviations from the reference, all reported by exceptions and never silent:
   by the payload string).  The engine models one sender per key and raises ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
   (crashed) replicas.
+
+Peers are identified as the shipped reference identifies them: by connection
+(``core/brbroadcast.py:69``; ``configure(peer_mode="sender")`` selects the commented-out :71
+line).  Best-effort broadcast keeps no peer sets, so its clusters ignore the setting.
 """
 import atexit
 import threading
@@ -34,13 +38,14 @@ from . import _lib as L
 
 _SETTINGS = {"delay_model": L.DELAY_CONST, "delay_max": 1, "delay_const": 1, "seed": 0,
              "round_cap": 3, "step_cap": 4000, "device": 0, "event_capacity": 1 << 20,
-             "instance_id": 0}
+             "instance_id": 0, "peer_mode": "connection"}
 _CLUSTERS = {}
 _LOCK = threading.Lock()
 _ATEXIT = [False]
 
 DELAY_MODELS = {"const": L.DELAY_CONST, "uniform": L.DELAY_UNIFORM, "slowset": L.DELAY_SLOWSET,
                 "geometric": L.DELAY_GEOMETRIC}
+PEER_MODES = {"connection": L.PEER_CONNECTION, "sender": L.PEER_SENDER}
 
 
 def configure(**kw):
@@ -48,10 +53,15 @@ def configure(**kw):
 
     delay_model ('const' | 'uniform' | 'slowset' | 'geometric' or a BRC_DELAY_* id), delay_max,
     delay_const, seed, round_cap, step_cap, device, event_capacity, instance_id (the global
-    instance id that keys the Philox schedule draws)."""
+    instance id that keys the Philox schedule draws), peer_mode ('connection', the default:
+    how the reference as shipped identifies peers, core/brbroadcast.py:69 -- every message is
+    its own connection, nothing is deduplicated and the :119 READY amplification re-fires; or
+    'sender', the commented-out :71 line)."""
     for k, v in kw.items():
         if k not in _SETTINGS:
             raise TypeError("unknown network setting %r" % k)
+        if k == "peer_mode" and v not in PEER_MODES:
+            raise ValueError("peer_mode must be 'connection' or 'sender', not %r" % (v,))
         if k == "delay_model" and isinstance(v, str):
             v = DELAY_MODELS[v]
         _SETTINGS[k] = v
@@ -218,7 +228,8 @@ class Cluster:
                              round_cap=c["round_cap"] if self.cons else 0, step_cap=c["step_cap"],
                              key_window=8, variants=1, byzantine=silent,
                              event_capacity=c["event_capacity"], instance_offset=c["instance_id"],
-                             device=c["device"], mode=L.MODE_BEB if self.beb else L.MODE_REFERENCE)
+                             device=c["device"], mode=L.MODE_BEB if self.beb else L.MODE_REFERENCE,
+                             peer_mode=L.PEER_SENDER if self.beb else PEER_MODES[c["peer_mode"]])
 
     def _flush(self):
         if self.actions:

@@ -57,7 +57,9 @@ enum { BRC_MODE_REFERENCE = 0, BRC_MODE_SPEC = 1, BRC_MODE_BEB = 2 };
  * network drops a message identical to one already sent on the link.  CONNECTION (:69, the
  * reference's local-test mode): every message is its own connection -- a new peer -- so sets
  * count messages, nothing is dropped, and the :119 amplification re-fires on every qualifying READY.
- * CONNECTION needs BRC_MODE_REFERENCE, n <= 64 and delay_max <= 8. */
+ * CONNECTION needs BRC_MODE_REFERENCE (any n <= 256, delay_max <= 16); it keeps per-cell send
+ * counts of one byte, so an injection of a 256th copy of one type by one replica in one step stops
+ * the instance with BRC_BADINJ. */
 enum { BRC_PEER_SENDER = 0, BRC_PEER_CONNECTION = 1 };
 enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DELAY_GEOMETRIC = 3 };
 enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };

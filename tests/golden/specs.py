@@ -246,6 +246,23 @@ def scenario_groups():
     G["conn_cons_byz_n16"] = [cons_spec(16, 5, 0x5EED0003, m, d, g, round_cap=1, byzantine=list(range(11, 16)), nv=2,
                                         extra=equivocation_actions(16, list(range(11, 16))), peer_mode="connection")
                               for (m, d) in ((1, 4), (2, 4)) for g in range(2)]
+    # the reference's own drivers (test/brb_test.py, test/brc_test.py) as they run: connection peers
+    G["conn_brb_fifo_n4"] = [clone(G["brb_fifo_n4"][0], peer_mode="connection", name="conn_brb_fifo_n4/0")]
+    G["conn_cons_brc_test_n6"] = [clone(G["cons_brc_test_n6"][0], peer_mode="connection",
+                                        name="conn_cons_brc_test_n6/0")]
+    G["conn_brb_uniform_n10"] = [brb_spec(10, 3, 1010, 1, 3, g, [(0, i, 0) for i in range(10)], peer_mode="connection")
+                                 for g in range(3)]
+    # ... on the wide kernel (n > 64) and with delays up to D = 16
+    G["conn_brb_uniform_n100"] = [brb_spec(100, 33, 0xC0AD, 1, 4, g, [(0, 0, 0), (0, 57, 0), (3, 99, 0)],
+                                           peer_mode="connection") for g in range(2)]
+    G["conn_brb_geometric_n128"] = [brb_spec(128, 42, 0xC0AE, 3, 16, g, [(0, 5, 0), (2, 100, 0)],
+                                             peer_mode="connection") for g in range(1)]
+    G["conn_brb_geometric_n16"] = [brb_spec(16, 5, 0xC0AF, 3, 12, g, [(0, i, 0) for i in range(0, 16, 3)],
+                                            peer_mode="connection") for g in range(3)]
+    G["conn_cons_geometric_n10"] = [cons_spec(10, 3, 0xC0B0, 3, 14, g, round_cap=2, peer_mode="connection")
+                                    for g in range(4)]
+    G["conn_cons_uniform_n100"] = [cons_spec(100, 33, 0xC0B1, 1, 4, g, round_cap=1, peer_mode="connection")
+                                   for g in range(1)]
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))

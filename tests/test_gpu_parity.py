@@ -96,14 +96,16 @@ def test_staggered_starts_vs_oracle(runner):
 
 
 # ---- connection-identity peers (core/brbroadcast.py:69) ----
-@pytest.mark.parametrize("n,f,model,dmax", [(4, 1, 1, 4), (7, 2, 3, 6), (16, 5, 2, 8), (33, 10, 1, 3), (64, 21, 2, 8)])
+@pytest.mark.parametrize("n,f,model,dmax", [(4, 1, 1, 4), (7, 2, 3, 6), (16, 5, 2, 8), (33, 10, 1, 3), (64, 21, 2, 8),
+                                             (16, 5, 3, 16), (64, 21, 1, 12),                 # D up to 16
+                                             (100, 33, 1, 4), (128, 42, 2, 8), (256, 85, 3, 16), (256, 85, 0, 3)])
 def test_connection_brb_floods_vs_oracle(runner, n, f, model, dmax):
     """Honest broadcasts plus Byzantine nodes that re-send ECHO / READY of honest keys at several
     steps: every copy is a new peer, so the counts (and K4 re-fires) differ from sender mode."""
     rng = random.Random(n * 31 + dmax)
     allm = (1 << n) - 1
     specs = []
-    for g in range(24 if n <= 16 else 6):
+    for g in range(24 if n <= 16 else 6 if n <= 64 else 3):
         byz = rng.sample(range(n), f)
         honest = [o for o in range(n) if o not in byz]
         sends = [(rng.randint(0, 3), o, 0) for o in rng.sample(honest, min(len(honest), 4))]
@@ -121,10 +123,11 @@ def test_connection_brb_floods_vs_oracle(runner, n, f, model, dmax):
 
 
 @pytest.mark.parametrize("n,f,model,dmax,rcap", [(4, 1, 1, 4, 3), (7, 2, 2, 4, 2), (10, 3, 3, 5, 2),
-                                                  (16, 5, 2, 8, 2), (64, 21, 2, 8, 1)])
+                                                  (16, 5, 2, 8, 2), (64, 21, 2, 8, 1), (10, 3, 3, 14, 2),
+                                                  (100, 33, 1, 4, 1), (128, 42, 2, 8, 1)])
 def test_connection_consensus_vs_oracle(runner, n, f, model, dmax, rcap):
     specs = []
-    for g in range(24 if n <= 16 else 4):
+    for g in range(24 if n <= 16 else 4 if n <= 64 else 1):
         sp = S.cons_spec(n, f, 0xC0C0 + n, model, dmax, 40 + g, round_cap=rcap, peer_mode="connection")
         sp["name"] = "conncons%d/%d" % (n, g)
         specs.append(sp)
@@ -140,3 +143,32 @@ def test_connection_equivocation_vs_oracle(runner):
         sp["name"] = "conncfg3/%d" % g
         specs.append(sp)
     _compare_with_oracle(runner, specs)
+
+
+@pytest.mark.parametrize("n,f,dmax", [(16, 5, 4), (100, 33, 4)])
+def test_connection_many_copies_vs_oracle(runner, n, f, dmax):
+    """Byzantine replicas re-send one READY / ECHO up to 255 times in one step (one-byte send
+    counts, 8 count planes): the arrival counts and the :119 re-fires they trigger match the
+    oracle."""
+    allm = (1 << n) - 1
+    byz = list(range(n - f, n))
+    specs = []
+    for g, copies in enumerate((40, 200, 255)):
+        extra = [dict(t=1, kind="byz", src=byz[0], type=3, kp=0, s=0, dst=allm) for _ in range(copies)]
+        extra += [dict(t=2, kind="byz", src=byz[1], type=2, kp=1, s=0, dst=allm) for _ in range(copies // 2)]
+        sp = S.brb_spec(n, f, 0xC0F0 + n, 1, dmax, 70 + g, [(0, 0, 0), (0, 1, 0)], byzantine=byz, extra=extra,
+                        peer_mode="connection")
+        sp["name"] = "copies%d/%d" % (n, copies)
+        specs.append(sp)
+    _compare_with_oracle(runner, specs)
+
+
+def test_connection_copy_count_ceiling_is_reported(runner):
+    """256 copies of one type from one replica in one step exceed the one-byte count: the
+    instance stops with bad_injection instead of miscounting."""
+    n, f = 16, 5
+    allm = (1 << n) - 1
+    extra = [dict(t=1, kind="byz", src=15, type=3, kp=0, s=0, dst=allm) for _ in range(256)]
+    sp = S.brb_spec(n, f, 0xC0F1, 1, 4, 5, [(0, 0, 0)], byzantine=[15], extra=extra, peer_mode="connection")
+    sp["name"] = "copies-ceiling"
+    assert runner.run_specs([sp])[0]["status"] == "bad_injection"

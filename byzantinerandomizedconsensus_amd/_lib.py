@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
 LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OK, E_INVALID, E_NOMEM, E_HIP, E_UNSUPPORTED, E_STATE = 0, -1, -2, -3, -4, -5
 ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP error",
@@ -63,7 +63,8 @@ class Config(ctypes.Structure):
 class Injection(ctypes.Structure):
     _fields_ = [("t", ctypes.c_uint32), ("kind", ctypes.c_uint16), ("type", ctypes.c_uint16),
                 ("instance", ctypes.c_uint64), ("node", ctypes.c_uint32), ("kp", ctypes.c_uint32),
-                ("s", ctypes.c_uint32), ("value", ctypes.c_int32), ("dst_mask", ctypes.c_uint64)]
+                ("s", ctypes.c_uint32), ("value", ctypes.c_int32), ("dst_mask", ctypes.c_uint64),
+                ("dst_mask_hi", ctypes.c_uint64 * 3)]
 
 
 class InstanceResult(ctypes.Structure):

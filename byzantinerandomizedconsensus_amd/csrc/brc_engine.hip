@@ -24,29 +24,33 @@ namespace {
 using namespace brc;
 
 // Byzantine equivocation pattern expanded straight into the CSR lists.
+// bw: Byzantine-mask words per instance (n > 64: one instance per item, ipw = 1)
 __global__ void expand_equivocate(InjDev* inj, uint32_t* off, uint32_t* cnt, const uint64_t* byz,
                                   uint64_t instances, uint64_t nitems, uint32_t ipw, uint32_t n, uint32_t nv,
-                                  uint32_t Q, uint32_t per_item) {
+                                  uint32_t Q, uint32_t per_item, uint32_t bw) {
     const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (item >= nitems) return;
     InjDev* o = inj + item * per_item;
     uint32_t c = 0;
-    uint64_t even = 0, odd = 0;
-    for (uint32_t dd = 0; dd < n; ++dd) { if (dd & 1) odd |= 1ull << dd; else even |= 1ull << dd; }
+    uint64_t even[4] = {0, 0, 0, 0}, odd[4] = {0, 0, 0, 0};   // 64 is even: bit parity = replica parity
+    for (uint32_t dd = 0; dd < n; ++dd) {
+        if (dd & 1) odd[dd >> 6] |= 1ull << (dd & 63); else even[dd >> 6] |= 1ull << (dd & 63);
+    }
     for (int pass = 0; pass < 2; ++pass) {
         for (uint32_t sgi = 0; sgi < ipw; ++sgi) {
             const uint64_t in = item * ipw + sgi;
             if (in >= instances) break;
-            const uint64_t bm = byz[in];
             for (uint32_t b = 0; b < n; ++b) {
-                if (!((bm >> b) & 1ull)) continue;
+                if (!((byz[in * bw + (b >> 6)] >> (b & 63)) & 1ull)) continue;
                 for (uint32_t v = 0; v < 2; ++v) {
                     const uint32_t kp = b * nv + v;
                     InjDev r = {};
                     r.slot = (uint16_t)(kp * Q + 0); r.s = 0; r.seg = (uint8_t)sgi; r.node = (uint8_t)b;
                     r.value = (int8_t)(1 + v);
                     if (pass == 0) {
-                        r.t = 0; r.kind = BRC_INJ_SEND; r.type = BRC_SEND; r.dst = v ? odd : even;
+                        r.t = 0; r.kind = BRC_INJ_SEND; r.type = BRC_SEND; r.restricted = 1;
+                        const uint64_t* dm = v ? odd : even;
+                        r.dst = dm[0]; r.dst_hi[0] = dm[1]; r.dst_hi[1] = dm[2]; r.dst_hi[2] = dm[3];
                         o[c++] = r;
                     } else {
                         r.t = 1; r.kind = BRC_INJ_MSG; r.dst = ~0ull;
@@ -294,7 +298,7 @@ static int apply_pattern(Engine* e) {
     const uint32_t blocks = (uint32_t)((e->nitems + 127) / 128);
     hipLaunchKernelGGL(expand_equivocate, dim3(blocks), dim3(128), 0, e->stream, e->inj, e->inj_off, e->inj_cnt,
                        e->byz, e->cfg.instances, e->nitems, (uint32_t)e->ipw, e->cfg.n, e->cfg.variants,
-                       e->cfg.key_window, cap);
+                       e->cfg.key_window, cap, e->bw);
     HIPCHK(e, hipGetLastError());
     e->pattern_active = true;
     return BRC_OK;
@@ -334,7 +338,7 @@ int brc_create(const brc_config* cfg, void** out) {
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
         c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB ||
-        (c.n > 64 && c.byz_pattern != BRC_BYZ_NONE) || (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
+        (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
     {
         g_create_err = "invalid configuration (see include/brc.h field ranges)";
         return BRC_E_INVALID;
@@ -384,7 +388,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, cells * 8}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
-        {(void**)&e->kdst, keys * 8}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * 8},
+        {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},
@@ -403,7 +407,7 @@ int brc_create(const brc_config* cfg, void** out) {
     }
     if (hipMemsetAsync(e->inj_off, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
-    if (hipMemsetAsync(e->kdst, 0, keys * 8, e->stream) != hipSuccess) return fail(BRC_E_HIP);
+    if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     {
         std::vector<uint64_t> bm((size_t)c.instances * e->bw);
         for (uint64_t i = 0; i < c.instances; ++i)
@@ -467,18 +471,20 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         r.t = x.t; r.kind = (uint8_t)x.kind; r.type = (uint8_t)x.type; r.node = (uint8_t)x.node;
         r.seg = (uint8_t)(x.instance % e->ipw); r.value = (int8_t)x.value; r.s = (uint16_t)x.s;
         r.dst = x.dst_mask & all;
+        bool full = (r.dst == word_mask(c.n, 0));
+        for (uint32_t w = 1; w < e->bw; ++w) {
+            r.dst_hi[w - 1] = x.dst_mask_hi[w - 1] & word_mask(c.n, w);
+            full = full && r.dst_hi[w - 1] == word_mask(c.n, w);
+        }
+        r.restricted = (x.kind == BRC_INJ_SEND && !full) ? 1 : 0;
         if (x.kind == BRC_INJ_PROPOSE) {
             if (c.protocol != BRC_PROTO_CONSENSUS) { e->err = "PROPOSE needs the consensus protocol"; return BRC_E_INVALID; }
         } else if (x.kind == BRC_INJ_SEND || x.kind == BRC_INJ_MSG || x.kind == BRC_INJ_KEY) {
             if (x.kp >= c.n * c.variants) { e->err = "kp out of range"; return BRC_E_INVALID; }
             r.slot = (uint16_t)(x.kp * c.key_window + (x.s % c.key_window));
-            if (e->wide && x.kind != BRC_INJ_KEY && x.dst_mask != ~0ull) {
-                e->err = "n > 64: SEND / ECHO / READY injections must address every peer (dst_mask = ~0)";
-                return BRC_E_UNSUPPORTED;
-            }
             if (x.kind == BRC_INJ_MSG) {
                 if (x.type != BRC_ECHO && x.type != BRC_READY) { e->err = "MSG type must be ECHO or READY"; return BRC_E_INVALID; }
-                if ((x.dst_mask & all) != all) { e->err = "ECHO/READY injections must address every peer"; return BRC_E_UNSUPPORTED; }
+                if (!full) { e->err = "ECHO/READY injections must address every peer"; return BRC_E_UNSUPPORTED; }
             } else if (x.kind == BRC_INJ_SEND) {
                 // one SEND per key: a second SEND (other sender / destinations) is not modelled
                 auto key = std::make_pair(x.instance, (uint32_t)(x.kp * 0x10000u + x.s));

@@ -45,13 +45,15 @@ constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, 
 #endif
 constexpr int CHUNK = BRC_CHUNK;            // narrow kernel: key slots whose cell loads are in flight together
 
-struct InjDev {       // 24 B, per item CSR, sorted by t
+struct InjDev {       // 48 B, per item CSR, sorted by t
     uint32_t t;
     uint16_t slot, s;
     uint8_t kind, type, seg, node;
     int8_t value;
-    uint8_t pad[3];
-    uint64_t dst;
+    uint8_t restricted;   // SEND to a strict subset of the peers (set by the host for n > 64)
+    uint8_t pad[2];
+    uint64_t dst;         // destinations 0..63 (the narrow kernel reads the first 24 B only)
+    uint64_t dst_hi[3];   // destinations 64..255 (wide kernel)
 };
 
 struct ItemState { uint32_t t, inj_pos, initialized, pad; };

@@ -95,11 +95,13 @@ template <typename T> using gptr_t = __attribute__((address_space(1))) T*;
 template <typename T> __device__ __forceinline__ gptr_t<T> gp(T* p) { return (gptr_t<T>)p; }
 
 // one 24-B injection record through global (not flat) loads
+// the first 24 B of a record (everything but dst_hi, which only the wide kernel reads)
 __device__ __forceinline__ InjDev load_inj(const InjDev* p) {
     const gptr_t<const uint64_t> q = gp((const uint64_t*)p);
     const uint64_t w[3] = {q[0], q[1], q[2]};
     InjDev r;
-    __builtin_memcpy(&r, w, sizeof(r));
+    __builtin_memcpy(&r, w, 24);
+    r.dst_hi[0] = r.dst_hi[1] = r.dst_hi[2] = 0;
     return r;
 }
 

@@ -424,10 +424,14 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                     if constexpr (SPEC) spec_advance(false);
                 }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
-                // every peer is a destination (brc_inject rejects restricted SENDs for n > 64)
                 const bool is_send = r.kind == BRC_INJ_SEND;
+                // restricted SEND (equivocation): this wave's word of the destination set, kept per
+                // key in kdst for the arrival test; each wave writes and reads only its own word
+                const bool restricted = is_send && r.restricted;
+                const uint64_t dw = restricted ? gp((const uint64_t*)(P.inj + inj_off + inj_pos - 1))[2 + wid] : ~0ull;
                 uint32_t myset = 0;
-                if (is_send && mine && honest) myset = 1u << (link_delay(r.node) - 1);
+                if (is_send && mine && honest && ((dw >> lane) & 1ull)) myset = 1u << (link_delay(r.node) - 1);
+                if (restricted && mine && lane == 0) gp(P.kdst)[(inst * NK + r.slot) * NW + wid] = dw;
                 const uint32_t os = block_or(myset);
                 if (mine) {
                     const uint32_t k = r.slot;
@@ -443,11 +447,18 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[k] = m;
-                            s_gen[k] = (uint16_t)gen;
+                            s_gen[k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 mark_lane(k, os);
-                                st_msgs += n;
+                                uint32_t nd = n;                 // links the SEND travels on
+                                if (restricted) {
+                                    const gptr_t<const uint64_t> rw = gp((const uint64_t*)(P.inj + inj_off + inj_pos - 1));
+                                    nd = 0;
+#pragma unroll
+                                    for (int w = 0; w < NW; ++w) nd += (uint32_t)__popcll(rw[2 + w]);
+                                }
+                                st_msgs += nd;
                                 log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
                             }
                         }
@@ -726,7 +737,11 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             bool s_arr = false;
             const uint32_t dt = t - m_tsend(m);
             const bool s_win = kl && dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);   // uniform
-            if (s_win) s_arr = honest && link_delay(m_sender(m)) == dt;
+            if (s_win) {
+                bool hit = link_delay(m_sender(m)) == dt;
+                if (gw & GEN16_RESTRICTED) hit = hit && ((gp(P.kdst)[(inst * NK + k) * NW + wid] >> lane) & 1ull);
+                s_arr = honest && hit;
+            }
             const bool has = kl && honest && (s_arr || ea || ra);
             st_loads += (kl && real) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 255, rc = (uint32_t)(word >> 13) & 255;

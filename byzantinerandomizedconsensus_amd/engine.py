@@ -96,9 +96,10 @@ class Engine:
             a.kp = x.get("kp", 0)
             a.s = x.get("s", 0)
             a.value = x.get("value", 0)
-            dst = x.get("dst", 0)
-            # n > 64: the engine takes only "every peer" destinations, spelled ~0
-            a.dst_mask = M64 if (self.n > 64 and dst == (1 << self.n) - 1) else dst & M64
+            dst = x.get("dst", 0)                  # bit d = replica d (n up to 256)
+            a.dst_mask = dst & M64
+            for w in range(3):
+                a.dst_mask_hi[w] = (dst >> (64 * (w + 1))) & M64
         self._chk(self._lib.brc_inject(self._h, arr, len(items)))
 
     # ------------------------------------------------------------------ execution

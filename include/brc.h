@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 3
+#define BRC_ABI_VERSION 4
 
 enum {
     BRC_OK = 0,
@@ -103,9 +103,13 @@ typedef struct {
     uint32_t node;            /* proposer / sender */
     uint32_t kp;              /* key slot: origin * variants + variant */
     uint32_t s;               /* phase index 2*(round-1)+(phase-1), or BRB sequence */
-    int32_t value;            /* value id (0 == "-1") */
-    uint64_t dst_mask;        /* BRC_INJ_SEND destinations; BRC_INJ_MSG must be all peers.
-                                 n > 64: both must be ~0 (every peer) */
+    int32_t value;            /* value id 0..3 (0 == "-1"; larger: BRC_E_INVALID -- two-bit ids, at most
+                                 three distinct proposal values besides "-1") */
+    uint64_t dst_mask;        /* BRC_INJ_SEND destinations 0..63; BRC_INJ_MSG must address all
+                                 peers (a restricted ECHO / READY: BRC_E_UNSUPPORTED).  A key is
+                                 SENT once: a second SEND of it (another origin, as one payload
+                                 string SENT by two nodes would be) is BRC_E_UNSUPPORTED */
+    uint64_t dst_mask_hi[3];  /* destinations 64..255 (n > 64), as byzantine_mask_hi */
 } brc_injection;
 
 typedef struct {

@@ -51,7 +51,7 @@ PROBE = r"""
 int main(void) {
   S(brc_config) S(brc_injection) S(brc_instance_result) S(brc_replica_result) S(brc_event) S(brc_stats)
   O(brc_config, seed) O(brc_config, byzantine_mask) O(brc_config, device)
-  O(brc_injection, instance) O(brc_injection, dst_mask) O(brc_event, a) O(brc_instance_result, msgs_sent)
+  O(brc_injection, instance) O(brc_injection, dst_mask) O(brc_injection, dst_mask_hi) O(brc_event, a) O(brc_instance_result, msgs_sent)
   return 0;
 }
 """
@@ -69,7 +69,8 @@ def test_struct_layouts_match_header():
         assert int(out[name]) == ctypes.sizeof(cls), name
     offs = {"brc_config.seed": L.Config.seed, "brc_config.byzantine_mask": L.Config.byzantine_mask,
             "brc_config.device": L.Config.device, "brc_injection.instance": L.Injection.instance,
-            "brc_injection.dst_mask": L.Injection.dst_mask, "brc_event.a": L.Event.a,
+            "brc_injection.dst_mask": L.Injection.dst_mask, "brc_injection.dst_mask_hi": L.Injection.dst_mask_hi,
+            "brc_event.a": L.Event.a,
             "brc_instance_result.msgs_sent": L.InstanceResult.msgs_sent}
     for name, field in offs.items():
         assert int(out[name]) == field.offset, name

@@ -23,7 +23,7 @@ DELAY_CONST, DELAY_UNIFORM, DELAY_SLOWSET, DELAY_GEOMETRIC = 0, 1, 2, 3
 PROPOSALS_NONE, PROPOSALS_PHILOX, PROPOSALS_LOADED = 0, 1, 2
 BYZ_NONE, BYZ_EQUIVOCATE = 0, 1
 SEND, ECHO, READY = 1, 2, 3
-INJ_PROPOSE, INJ_SEND, INJ_KEY, INJ_MSG = 1, 2, 3, 4
+INJ_PROPOSE, INJ_SEND, INJ_KEY, INJ_MSG, INJ_DELIVER = 1, 2, 3, 4, 5
 RUNNING, DONE, QUIESCENT, STEPCAP, OVERFLOW, BADINJ = 0, 1, 2, 3, 4, 5
 STATUS_NAMES = {RUNNING: "running", DONE: "done", QUIESCENT: "quiescent", STEPCAP: "stepcap",
                 OVERFLOW: "overflow", BADINJ: "bad_injection"}

@@ -6,6 +6,7 @@ keeps the reference's constructor (note the argument order: ``peer_list`` before
 ``host_address``), ``message_queue``, ``start``/``propose`` and the ``decide`` upcall to
 ``consensus_user`` (:94).
 """
+import json
 import queue
 
 from ..base.broadcast import IBroadcastHandler
@@ -43,6 +44,10 @@ class ByzantineRandomizedConsensus(Consensus, IBroadcastHandler):
         print("Proposal sent on " + str(self.host_address))
 
     def deliver(self, message):
-        """BRB deliveries are consumed by the engine's consensus pass; there is no host-side
-        delivery path to call into."""
-        raise NotImplementedError("deliveries are processed inside the engine")
+        """The IBroadcastHandler upcall (:53).  BRB deliveries of the cluster's own traffic are
+        consumed inside the engine; a direct call -- a JSON message as the reference builds it
+        (:48-49), {"host": address, "round": r, "phase": p, "message": value} -- is handed to this
+        replica's consensus state at the cluster's current step (round and phase are not read,
+        as in the reference)."""
+        d = json.loads(message)
+        self.brb.cluster.deliver(self.brb.node_id, tuple(d["host"]), str(d["message"]))

@@ -479,6 +479,11 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         r.restricted = (x.kind == BRC_INJ_SEND && !full) ? 1 : 0;
         if (x.kind == BRC_INJ_PROPOSE) {
             if (c.protocol != BRC_PROTO_CONSENSUS) { e->err = "PROPOSE needs the consensus protocol"; return BRC_E_INVALID; }
+        } else if (x.kind == BRC_INJ_DELIVER) {
+            if (c.protocol != BRC_PROTO_CONSENSUS) { e->err = "DELIVER needs the consensus protocol"; return BRC_E_INVALID; }
+            if (c.mode == BRC_MODE_SPEC) { e->err = "DELIVER: SPEC consensus counts phase-indexed keys"; return BRC_E_UNSUPPORTED; }
+            if (x.kp >= c.n) { e->err = "DELIVER host out of range"; return BRC_E_INVALID; }
+            r.slot = (uint16_t)x.kp;               // the message's host
         } else if (x.kind == BRC_INJ_SEND || x.kind == BRC_INJ_MSG || x.kind == BRC_INJ_KEY) {
             if (x.kp >= c.n * c.variants) { e->err = "kp out of range"; return BRC_E_INVALID; }
             r.slot = (uint16_t)(x.kp * c.key_window + (x.s % c.key_window));

@@ -493,8 +493,8 @@ void brc_step(const Params* __restrict__ pp) {
         vcount = 0; nvals = 0; order = 0;
         for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
     };
-    auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = (uint32_t)s_snap[mbase + k] >> 14, host = k >> ksh;   // snapshot (see s_snap)
+    // :53-106 for a message of `host` carrying value id v (a BRB delivery, or BRC_INJ_DELIVER)
+    auto cons_deliver_vh = [&](uint32_t v, uint32_t host) {
         // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
         const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
         const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
@@ -517,6 +517,9 @@ void brc_step(const Params* __restrict__ pp) {
             ++round; phase = 1; cons_reset();                        // :96-100
             send_key(2 * (round - 1), dec);                          // :102-106
         }
+    };
+    auto cons_deliver = [&](uint32_t k) {
+        cons_deliver_vh((uint32_t)s_snap[mbase + k] >> 14, k >> ksh);   // snapshot (see s_snap)
     };
 
     // ---- SPEC consensus (oracle spec_advance / spec_deliver): the protocol
@@ -593,6 +596,11 @@ void brc_step(const Params* __restrict__ pp) {
                 if (mine && honest && d == r.node) {
                     round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
                     if constexpr (SPEC) spec_advance();
+                }
+            } else if (r.kind == BRC_INJ_DELIVER) {
+                // a direct deliver() call (brc_inject refuses it for SPEC): host in r.slot
+                if constexpr (!SPEC) {
+                    if (mine && honest && d == r.node) cons_deliver_vh((uint32_t)r.value & 3, r.slot);
                 }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the

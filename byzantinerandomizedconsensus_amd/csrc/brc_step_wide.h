@@ -335,8 +335,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
         for (uint32_t v = 0; v < 4; ++v)
             for (uint32_t w = 0; w < NW; ++w) hm(v, w) = 0;
     };
-    auto cons_deliver = [&](uint32_t k) {                            // :53-106
-        const uint32_t v = m_value(s_meta[k]) & 3, host = k >> ksh;
+    // :53-106 for a message of `host` carrying value id v (a BRB delivery, or BRC_INJ_DELIVER)
+    auto cons_deliver_vh = [&](uint32_t v, uint32_t host, bool defer) {
         // v already inserted? every 2-bit field of `order` compared at once (nvals <= 4)
         const uint32_t x = order ^ (v * 0x55u);
         const bool found = (~(x | (x >> 1)) & 0x55u & ((1u << (2 * nvals)) - 1u)) != 0;
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
         if (vcount >= P.T_cnt && phase == 1) {                       // :71
             const uint32_t prop = get_max_val(P.bound_p1);           // :73
             phase = 2; cons_reset();                                 // :75-78
-            send_later(2 * (round - 1) + 1, prop);                   // :80-83
+            if (defer) send_later(2 * (round - 1) + 1, prop); else send_key(2 * (round - 1) + 1, prop);   // :80-83
         }
         if (vcount >= P.T_cnt && phase == 2) {                       // :86
             const uint32_t dec = get_max_val(P.bound_p2);            // :88
@@ -355,9 +355,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             lval = dec;
             log_ev(BRC_EV_DECIDE, d, 0, round, dec, dec);
             ++round; phase = 1; cons_reset();                        // :96-100
-            send_later(2 * (round - 1), dec);                        // :102-106
+            if (defer) send_later(2 * (round - 1), dec); else send_key(2 * (round - 1), dec);   // :102-106
         }
     };
+    auto cons_deliver = [&](uint32_t k) { cons_deliver_vh(m_value(s_meta[k]) & 3, k >> ksh, true); };
 
     // ---- SPEC consensus (as brc_step.h spec_advance / spec_deliver)
     auto spec_advance = [&](bool defer) {
@@ -422,6 +423,11 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                 if (mine && honest && d == r.node) {
                     round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
                     if constexpr (SPEC) spec_advance(false);
+                }
+            } else if (r.kind == BRC_INJ_DELIVER) {
+                // a direct deliver() call (brc_inject refuses it for SPEC): host in r.slot
+                if constexpr (!SPEC) {
+                    if (mine && honest && d == r.node) cons_deliver_vh((uint32_t)r.value & 3, r.slot, false);
                 }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 const bool is_send = r.kind == BRC_INJ_SEND;

@@ -214,6 +214,16 @@ class Cluster:
         """ByzantineRandomizedConsensus.propose (core/byzantinerandomizedconsensus.py:43-50)."""
         self.actions.append(dict(t=self.t, kind=L.INJ_PROPOSE, node=i, value=self.values.id_of(message)))
 
+    def deliver(self, i, host, message):
+        """ByzantineRandomizedConsensus.deliver called directly on replica i with a message of
+        `host` (a peer address) carrying `message` (core/byzantinerandomizedconsensus.py:53-106):
+        the replica's consensus state takes it at the current step, without BRB traffic."""
+        h = _addr(host)
+        if h not in self.index:
+            raise L.EngineError(L.E_UNSUPPORTED, "deliver(): host %r is not in the peer list" % (h,))
+        self.actions.append(dict(t=self.t, kind=L.INJ_DELIVER, node=i, kp=self.index[h],
+                                 value=self.values.id_of(message)))
+
     # ------------------------------------------------------------------ execution
     def _create_engine(self):
         from .engine import Engine

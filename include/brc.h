@@ -65,7 +65,11 @@ enum { BRC_DELAY_CONST = 0, BRC_DELAY_UNIFORM = 1, BRC_DELAY_SLOWSET = 2, BRC_DE
 enum { BRC_PROPOSALS_NONE = 0, BRC_PROPOSALS_PHILOX = 1, BRC_PROPOSALS_LOADED = 2 };
 enum { BRC_BYZ_NONE = 0, BRC_BYZ_EQUIVOCATE = 1 };
 enum { BRC_SEND = 1, BRC_ECHO = 2, BRC_READY = 3 };
-enum { BRC_INJ_PROPOSE = 1, BRC_INJ_SEND = 2, BRC_INJ_KEY = 3, BRC_INJ_MSG = 4 };
+/* BRC_INJ_DELIVER: ByzantineRandomizedConsensus.deliver(message) called directly on replica `node`
+ * (core/byzantinerandomizedconsensus.py:53) with a message of host `kp` (a replica id) carrying
+ * value id `value` -- no BRB traffic; the consensus logic runs as on a BRB delivery.  Consensus
+ * protocol, BRC_MODE_REFERENCE or BRC_MODE_BEB (BRC_MODE_SPEC counts phases: BRC_E_UNSUPPORTED). */
+enum { BRC_INJ_PROPOSE = 1, BRC_INJ_SEND = 2, BRC_INJ_KEY = 3, BRC_INJ_MSG = 4, BRC_INJ_DELIVER = 5 };
 enum { BRC_RUNNING = 0, BRC_DONE = 1, BRC_QUIESCENT = 2, BRC_STEPCAP = 3, BRC_OVERFLOW = 4, BRC_BADINJ = 5 };
 enum { BRC_EV_DELIVER = 1, BRC_EV_DECIDE = 2, BRC_EV_SEND = 3 };
 

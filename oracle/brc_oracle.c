@@ -243,12 +243,11 @@ static void cons_reset(cons_t* c) {
 }
 
 /* core/byzantinerandomizedconsensus.py:53-106 */
-static void cons_deliver(sim_t* S, uint32_t node, int key) {
+/* core/byzantinerandomizedconsensus.py:53-106 at replica `node` for a message of `host` carrying
+ * value id v (the BRB deliver upcall, or a direct deliver() call: OR_ACT_DELIVER) */
+static void cons_deliver_vh(sim_t* S, uint32_t node, int32_t v, uint32_t host) {
     cons_t* c = &S->cons[node];
-    key_t_* k = &S->keys[key];
-    int32_t v = k->value;
-    uint32_t host = k->kp / S->sp->nv;            /* frozenset(dict["host"]) (:55) */
-    if (v < 0 || v >= NVAL) { S->err = -6; return; }
+    if (v < 0 || v >= NVAL || host >= S->n) { S->err = -6; return; }
     uint32_t i;
     for (i = 0; i < c->nvals; ++i) if (c->order[i] == v) break;
     if (i == c->nvals) c->order[c->nvals++] = v;   /* :57-58 */
@@ -273,6 +272,11 @@ static void cons_deliver(sim_t* S, uint32_t node, int key) {
         cons_reset(c);                             /* :98-100 */
         cons_send_key(S, node, 2 * (c->round - 1), dec);        /* :102-106 */
     }
+}
+
+static void cons_deliver(sim_t* S, uint32_t node, int key) {
+    const key_t_* k = &S->keys[key];
+    cons_deliver_vh(S, node, k->value, k->kp / S->sp->nv);   /* host: frozenset(dict["host"]) (:55) */
 }
 
 /* ------------------------------------------------------------------ SPEC consensus */
@@ -452,6 +456,11 @@ static void do_action(sim_t* S, const oracle_action* a) {
     }
     case OR_ACT_BYZ_KEY:
         key_get(S, a->kp, a->s, a->value);
+        break;
+    case OR_ACT_DELIVER:                      /* a direct deliver() call (:53): no BRB involved */
+        if (a->node >= S->n || !is_honest(S, a->node) ||
+            (S->sp->mode != OR_MODE_CONSENSUS && S->sp->mode != OR_MODE_BEB_CONSENSUS)) { S->err = -9; return; }
+        cons_deliver_vh(S, a->node, a->value, a->kp);
         break;
     case OR_ACT_BYZ: {
         int key = key_find(S, a->kp, a->s);

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "liboracle.so")
 
-ACT = {"propose": 1, "brb_send": 2, "byz_key": 3, "byz": 4}
+ACT = {"propose": 1, "brb_send": 2, "byz_key": 3, "byz": 4, "deliver": 5}
 STATUS = {1: "done", 2: "quiescent", 3: "stepcap", 4: "overflow"}
 PEER_MODES = {"sender": 0, "connection": 1}
 MODES = {"brb": 0, "consensus": 1, "spec": 2, "spec_brb": 3, "beb": 4, "beb_consensus": 5}

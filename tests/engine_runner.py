@@ -38,6 +38,9 @@ def _injections(sp, local):
         elif k == "brb_send":
             out.append(dict(t=a["t"], kind=L.INJ_SEND, instance=local, node=a["node"], kp=a["kp"], s=a["s"],
                             value=a.get("value", 0), dst=allm))
+        elif k == "deliver":               # ByzantineRandomizedConsensus.deliver() called directly
+            out.append(dict(t=a["t"], kind=L.INJ_DELIVER, instance=local, node=a["node"], kp=a["kp"],
+                            value=a["value"]))
         elif k == "byz_key":
             values[(a["kp"], a["s"])] = a.get("value", 0)
             out.append(dict(t=a["t"], kind=L.INJ_KEY, instance=local, node=a["kp"] // nv, kp=a["kp"], s=a["s"],

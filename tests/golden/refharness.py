@@ -339,6 +339,9 @@ class Run:
             self.register(payload, key)
         elif kind == "byz":
             self.byz_send(a["src"], a["type"], (a["kp"], a["s"]), a["dst"])
+        elif kind == "deliver":       # ByzantineRandomizedConsensus.deliver(message) called directly
+            msg = consensus_payload(self.addrs[a["kp"]], a.get("round", 1), a.get("phase", 1), self.values[a["value"]])
+            self.nodes[a["node"]].deliver(msg)
         else:
             raise HarnessError("unknown action %r" % kind)
 

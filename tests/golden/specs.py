@@ -14,6 +14,7 @@ actions (each performed after step ``t`` is processed, messages stamped ``t``):
     {"kind": "byz",      "t", "src", "type", "kp", "s", "dst"}   raw Byzantine message(s)
 """
 import copy
+import random
 
 VALUES = ["-1", "0", "1", "3"]
 SEND, ECHO, READY = 1, 2, 3
@@ -97,6 +98,14 @@ def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
             acts.append(dict(t=t_er, kind="byz", src=b, type=ECHO, kp=b * nv + v, s=0, dst=allm))
             acts.append(dict(t=t_er, kind="byz", src=b, type=READY, kp=b * nv + v, s=0, dst=allm))
     return acts
+
+
+def deliver_actions(n, seed, count=None):
+    """Direct deliver() calls: replica `node` is handed host `kp`'s message with value id `value`
+    at step t (an action: after step t's messages)."""
+    rng = random.Random(seed)
+    return [dict(t=rng.randint(0, 8), kind="deliver", node=rng.randrange(n), kp=rng.randrange(n),
+                 value=rng.randint(0, 3)) for _ in range(count or 2 * n)]
 
 
 def _kat(n, f, seq, byz_nodes, key=(1, 0), name=""):
@@ -246,6 +255,12 @@ def scenario_groups():
     G["conn_cons_byz_n16"] = [cons_spec(16, 5, 0x5EED0003, m, d, g, round_cap=1, byzantine=list(range(11, 16)), nv=2,
                                         extra=equivocation_actions(16, list(range(11, 16))), peer_mode="connection")
                               for (m, d) in ((1, 4), (2, 4)) for g in range(2)]
+    # ByzantineRandomizedConsensus.deliver(message) called directly (core/byzantinerandomizedconsensus.py:53):
+    # extra values from chosen hosts, some before the replica's own proposal (phase 0: counted only)
+    G["cons_deliver_n6"] = [cons_spec(6, 1, 0xDE10, m, d, g, round_cap=2, starts=[0, 0, 0, 3, 0, 6],
+                                      extra=deliver_actions(6, 0xDE10 + g)) for (m, d) in ((0, 1), (1, 3)) for g in range(3)]
+    G["cons_deliver_n16"] = [cons_spec(16, 3, 0xDE20, 2, 4, g, round_cap=1, extra=deliver_actions(16, 0xDE20 + g))
+                             for g in range(2)]
     # the reference's own drivers (test/brb_test.py, test/brc_test.py) as they run: connection peers
     G["conn_brb_fifo_n4"] = [clone(G["brb_fifo_n4"][0], peer_mode="connection", name="conn_brb_fifo_n4/0")]
     G["conn_cons_brc_test_n6"] = [clone(G["cons_brc_test_n6"][0], peer_mode="connection",

@@ -129,3 +129,17 @@ def test_rejections_are_documented_error_codes(n):
         with pytest.raises(L.EngineError) as ei:
             eng.inject([dict(t=0, kind=L.INJ_PROPOSE, node=0, value=4)])
         assert ei.value.code == L.E_INVALID
+
+
+@pytest.mark.parametrize("n,f,model,dmax", [(7, 1, 1, 3), (100, 19, 0, 1), (128, 25, 2, 4)])
+def test_direct_deliver_vs_oracle(runner, n, f, model, dmax):
+    """ByzantineRandomizedConsensus.deliver() called directly (BRC_INJ_DELIVER) on the narrow and
+    the wide kernel: random hosts and values, before and after the replicas' own proposals."""
+    specs = []
+    for g in range(2):
+        sp = S.cons_spec(n, f, 0xDE40 + n, model, dmax, 10 + g, round_cap=2,
+                         starts=[(d * 7 + g) % 4 for d in range(n)],
+                         extra=S.deliver_actions(n, 0xDE40 + n + g, count=3 * n))
+        sp["name"] = "deliver%d/%d" % (n, g)
+        specs.append(sp)
+    _compare(runner, specs)

@@ -195,7 +195,8 @@ class Run:
         self.servers = {}
         self.t = 0
         self.arrivals = defaultdict(list)
-        self.sent = set()
+        self.sent = defaultdict(int)    # (src, type, kp, s) -> destinations already sent to (bit mask)
+        self.keep_wire = spec.get("keep_wire", True)   # large runs: no per-message wire log
         self.first_sends = set()
         self.key_of_payload = {}
         self.payload_of_key = {}
@@ -240,13 +241,14 @@ class Run:
         env = json.loads(data.decode("utf-8"))
         payload, mtype = env["message"], env["type"]
         kp, s = self.key_for(payload)
-        ident = (src, dst, mtype, payload)
         if not self.connection:
-            if ident in self.sent:      # duplicate-suppressing network (sender-identity peers)
+            ident = (src, mtype, kp, s)  # one payload per key (register() checks)
+            if (self.sent[ident] >> dst) & 1:   # duplicate-suppressing network (sender-identity peers)
                 return
-            self.sent.add(ident)
+            self.sent[ident] |= 1 << dst
         self.msgs_sent += 1
-        self.wire.append([self.t, src, dst, data.decode("utf-8")])
+        if self.keep_wire:
+            self.wire.append([self.t, src, dst, data.decode("utf-8")])
         fs = (src, mtype, payload)
         if fs not in self.first_sends:
             self.first_sends.add(fs)

@@ -242,7 +242,8 @@ def scenario_groups():
     G["cons_slowset_n70"] = [cons_spec(70, 23, 0x5EED0005, 2, 8, g, round_cap=1) for g in range(1)]
     # reference-protocol consensus on the wide kernel's committees (SURVEY §8(d) cfg5 sizes)
     G["cons_slowset_n128"] = [cons_spec(128, 42, 0x5EED0005, 2, 8, g, round_cap=1) for g in range(1)]
-    G["cons_slowset_n256"] = [cons_spec(256, 85, 0x5EED0005, 2, 8, g, round_cap=1) for g in range(1)]
+    G["cons_slowset_n256"] = [dict(cons_spec(256, 85, 0x5EED0005, 2, 8, g, round_cap=1), keep_wire=False)
+                              for g in range(1)]
     # connection-identity peers (core/brbroadcast.py:69, the reference's local-test mode)
     G["conn_kat"] = [clone(sp, peer_mode="connection", name=sp["name"] + "-conn")
                      for sp in kat_specs().values()]

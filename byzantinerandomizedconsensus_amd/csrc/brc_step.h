@@ -251,7 +251,9 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 // metadata read once per chunk, exec-masked cell stores and (NLR = 2) link-delay masks held in
 // registers -- the headline configuration has exactly two link delays.
 #ifdef BRC_STAMPS
-__device__ unsigned long long brc_stamps[4];   // dev-only section timers (s_memtime ticks)
+// dev-only: [0..3] section timers (s_memtime ticks); [4..7] lean key-steps: processed, without
+// arrivals, reaching only delivered cells, fully updated
+__device__ unsigned long long brc_stamps[8];
 #endif
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
 
@@ -712,10 +714,13 @@ void brc_step(const Params* __restrict__ pp) {
 
 #ifdef BRC_STAMPS
     uint64_t stamp_acc[4] = {0, 0, 0, 0};
+    uint32_t kcount[4] = {0, 0, 0, 0};
     uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
 #define BRC_STAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
+#define BRC_KCOUNT(i) (++kcount[i])
 #else
 #define BRC_STAMP(i) do {} while (0)
+#define BRC_KCOUNT(i) do {} while (0)
 #endif
     for (uint32_t it = 0; it < P.max_steps; ++it) {
         const bool running0 = status == BRC_RUNNING;
@@ -768,6 +773,7 @@ void brc_step(const Params* __restrict__ pp) {
             const uint32_t gen = gw & GEN_MASK;
             if (m_s1(m) == 0) return;                            // the slot holds no key
             ++nk_lean;                                           // lane loads: one word per real lane
+            BRC_KCOUNT(0);
             const uint32_t wlo = (uint32_t)wd, whi = (uint32_t)(wd >> 32);
             // a stale word (older generation) is a fresh cell: lanes that are not real replicas
             // and Byzantine lanes never store here, so their words read "never sent"
@@ -783,8 +789,10 @@ void brc_step(const Params* __restrict__ pp) {
                 // nothing), so each count is ONE popcount of a bitfield merge (v_bfi)
                 const uint64_t be0 = __ballot(tE == tm0), br0 = __ballot(tR == tm0);
                 const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
-                ea = popc((be0 & RL0) | (be1 & ~RL0));
-                ra = popc((br0 & RL0) | (br1 & ~RL0));
+                // (b0 & RL0) | (b1 & ~RL0) == b1 ^ ((b0 ^ b1) & RL0): the XOR of the two ballots is
+                // scalar, leaving two VALU ops per 32-bit half (-0.45 % kernel, A/B)
+                ea = popc(be1 ^ ((be0 ^ be1) & RL0));
+                ra = popc(br1 ^ ((br0 ^ br1) & RL0));
                 be_any = be0 | be1; br_any = br0 | br1;
             } else {
                 const uint32_t dE = t - tE, dR = t - tR;
@@ -820,14 +828,15 @@ void brc_step(const Params* __restrict__ pp) {
                 s_arr = honest && hit;
             }
             const bool has = honest && (s_arr || ea || ra);
-            if (!__ballot(has)) return;                          // nothing lands on this key now
+            if (!__ballot(has)) { BRC_KCOUNT(1); return; }      // nothing lands on this key now
             // Per-lane work below is branch-free integer arithmetic on 0/1 flags: lane-mask logic
             // and divergent branches would cost scalar (SALU) instructions, the busier issue port.
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;
             // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
             const bool opn = has && !(lo & F_DEL);
-            if (!__ballot(opn)) return;
+            if (!__ballot(opn)) { BRC_KCOUNT(2); return; }
+            BRC_KCOUNT(3);
             uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
             uint32_t es = 0, rs = 0, dl = 0;                     // 0/1: ECHO sent, READY sent, delivered
             const uint32_t sa = (opn && s_arr) ? 1u : 0u;
@@ -1187,6 +1196,7 @@ void brc_step(const Params* __restrict__ pp) {
 
 #ifdef BRC_STAMPS
     if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[4 + i], (unsigned long long)kcount[i]);
 #endif
 #undef BRC_STAMP
     // ---- write back

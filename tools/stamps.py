@@ -14,13 +14,16 @@ inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
 eng = Engine(n=64, f=21, instances=inst, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET,
              delay_max=8, round_cap=1, step_cap=4000, key_window=4, variants=1, proposals=L.PROPOSALS_PHILOX)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
-out = (ctypes.c_ulonglong * 4)()
+out = (ctypes.c_ulonglong * 8)()
 eng.reset(); eng.run()
 lib.brc_dbg_stamps(out)
 eng.reset(); eng.run()
 lib.brc_dbg_stamps(out)
-tot = sum(out)
+tot = sum(out[:4])
 names = ["step head + key list", "key loop (BRB cells)", "consensus deliveries", "actions + stop checks"]
-for nm, v in zip(names, out):
+for nm, v in zip(names, out[:4]):
     print("%-24s %6.1f %%  (%.3g ticks)" % (nm, 100.0 * v / tot, v))
+kn = ["key-steps processed", "  no arrivals", "  only delivered cells", "  updated"]
+for nm, v in zip(kn, out[4:]):
+    print("%-24s %.4g  (%.1f %%)" % (nm, v, 100.0 * v / max(1, out[4])))
 print("kernel ms %.2f" % eng.last_kernel_ms())

@@ -17,9 +17,10 @@ Two legs, one JSON line (rank 0):
              `value`.  Its coin branch is dead, so split proposals decide "-1" in
              round 1; `decided_value_hist` shows that share.
   spec       the protocol the reference intends, with the common coin made reachable (SURVEY §8
-             F3): "many coin rounds".  Its phase window Q = 8 doubles the cell footprint, so the
-             2^20 instances run as tiles of an engine re-keyed per tile (brc_reset_at): every timed
-             step covers all 2^20 instances; the statistics come from one extra untimed pass.
+             F3): "many coin rounds".  Its phase window Q = 8 doubles the key slots; with 4-B cells
+             2^20 instances still fit one engine (138 GB of cells), so it is one launch per step.
+             Larger counts run as tiles of an engine re-keyed per tile (brc_reset_at); the
+             statistics then come from one extra untimed pass.
 """
 import argparse
 import json
@@ -32,9 +33,10 @@ sys.path.insert(0, ROOT)
 
 N_REPLICAS, F_FAULTS, DELAY_MAX, SEED, COIN_SEED = 64, 21, 8, 0x5EED0004, 0xC017C017
 SURVEY_BYTES_PER_CELL_STEP = 6 * ((N_REPLICAS + 7) // 8) + 2   # 50 B at n=64
-FLOOR_BYTES_PER_CELL_STEP = 16                                  # this layout: 8-B cell word read + written
+CELL_BYTES = 4                                                  # lean kernels' compact cell (brc_internal.h C32_*)
+FLOOR_BYTES_PER_CELL_STEP = 2 * CELL_BYTES                      # this layout: the cell word read + written
 HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
-SPEC_TILE = 1 << 19                                             # SPEC (Q = 8) instances per engine tile
+SPEC_TILE = 1 << 20                                             # SPEC (Q = 8) instances per engine tile
 
 
 def parse():
@@ -107,7 +109,7 @@ def load_traffic(instances, kernel_ms, mode="reference"):
     except (OSError, ValueError):
         return None
     if d.get("instances") != instances or d.get("workload") != "cfg4" or not d.get("avg_ns") or \
-            d.get("mode", "reference") != mode:
+            d.get("mode", "reference") != mode or d.get("cell_bytes", 8) != CELL_BYTES:
         return None
     if abs(d["avg_ns"] / 1e6 - kernel_ms) > 0.15 * kernel_ms:
         return None
@@ -203,13 +205,13 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "traffic_frac": (traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-            "floor_frac": floor / HBM_PEAK_GBS,
+            "floor_frac": floor / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
             "note": "algorithmic = %d B (SURVEY 8(d)) x %d cell-steps per GPU per step (%d launch%s): it credits "
-                    "n-bit ECHO/READY masks this design never moves (one 8-B word per cell), so frac can pass 1; "
+                    "n-bit ECHO/READY masks this design never moves (one %d-B word per cell), so frac can pass 1; "
                     "the physical figures are floor_frac (%d B: the cell word read + written, per cell-step) and "
                     "traffic_frac (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json)"
                     % (SURVEY_BYTES_PER_CELL_STEP, cs_gpu, launches, "" if launches == 1 else "es",
-                       FLOOR_BYTES_PER_CELL_STEP)}
+                       CELL_BYTES, FLOOR_BYTES_PER_CELL_STEP)}
     leg = {
         "value": decided * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,

@@ -132,7 +132,7 @@ __global__ void decision_histogram(const uint64_t* cons1, const uint64_t* byz, u
 
 // grid-stride fill: a dispatch holds < 2^32 work-items per dimension, and the cell array can
 // exceed that (2^17 instances x 512 key slots x 64 lanes = 2^32 words at n = 64, Q = 8)
-__global__ void fill_u64(uint64_t* p, uint64_t v, uint64_t count) {
+template <typename W> __global__ void fill_words(W* p, W v, uint64_t count) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) p[i] = v;
 }
@@ -143,6 +143,7 @@ struct Engine {
     int npad = 0, dm = 0, ipw = 0, nkw_t = 0;
     bool wide = false;                           // n > 64: one workgroup per instance (brc_step_wide.h)
     bool regmask = false;                        // NPAD = 64 lean kernel with register delay masks (NLR = 2)
+    bool compact = false;                        // lean kernels (NPAD = 64, sender peers): u32 cells (C32_*)
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
@@ -227,7 +228,12 @@ static int clear_state(Engine* e, bool full) {
     const size_t keys = (size_t)e->cfg.instances * e->NK;
     if (full) {
         const uint64_t fb = std::min<uint64_t>((cells + 255) / 256, 1u << 20);
-        hipLaunchKernelGGL(fill_u64, dim3((uint32_t)fb), dim3(256), 0, e->stream, e->cells, TIMES_NEVER, (uint64_t)cells);
+        if (e->compact)
+            hipLaunchKernelGGL(fill_words<uint32_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, (uint32_t*)e->cells,
+                               C32_FRESH, (uint64_t)cells);
+        else
+            hipLaunchKernelGGL(fill_words<uint64_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, e->cells, TIMES_NEVER,
+                               (uint64_t)cells);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipMemsetAsync(e->meta, 0, keys * 8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->mgen, 0, keys * 4, e->stream));
@@ -364,6 +370,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
     e->regmask = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && nL <= 2;
+    e->compact = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER;   // = lean_kernel<64, mode> (brc_step.h)
     // wide exchange words per (key, type): connection peers send 8 count planes per link delay
     const uint32_t xw = c.peer_mode == BRC_PEER_CONNECTION ? 8u * nL : xwords_wide(c.delay_model, c.delay_max, e->dm);
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xw,
@@ -387,7 +394,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
-        {(void**)&e->cells, cells * 8}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
+        {(void**)&e->cells, cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
         {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},

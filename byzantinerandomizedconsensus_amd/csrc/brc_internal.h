@@ -56,7 +56,19 @@ struct InjDev {       // 48 B, per item CSR, sorted by t
     uint64_t dst_hi[3];   // destinations 64..255 (wide kernel)
 };
 
-struct ItemState { uint32_t t, inj_pos, initialized, pad; };
+// epoch: the lean kernels' send-step base (compact cells below); 0 elsewhere
+struct ItemState { uint32_t t, inj_pos, initialized, epoch; };
+
+// Compact cell of the lean kernels (NPAD = 64, sender peers: brc_step.h), one u32:
+//   bits 0-2 F_EEX, F_REX, F_DEL   bits 3-8 |echo set|   bits 9-14 |ready set| (both saturate at 63)
+//   bits 15-17 slot generation mod 8
+//   bits 18-24 / 25-31: step this lane SENT its ECHO / READY, as an offset from the item's epoch;
+//   C32_OLD = sent more than DM steps before the epoch, C32_NEVER = not sent
+constexpr uint32_t C32_GEN_SH = 15, C32_GEN = 7, C32_OE_SH = 18, C32_OR_SH = 25;
+constexpr uint32_t C32_NEVER = 127, C32_OLD = 126;
+constexpr uint32_t C32_FRESH = (C32_NEVER << C32_OE_SH) | (C32_NEVER << C32_OR_SH);   // generation 0
+constexpr uint32_t C32_REBASE = 100;   // a step more than this past the epoch moves the epoch first
+constexpr uint32_t C32_KEEP = 17;      // ... to t - C32_KEEP: sends in the last 16 steps keep their step
 
 struct InstState { uint16_t status, t_stop, q_until, flags; uint32_t pad0, pad1; };
 

@@ -315,6 +315,7 @@ void brc_step(const Params* __restrict__ pp) {
 
     ItemState its = P.items[item];
     uint32_t t = LEAN ? uni32(its.t) : its.t, inj_pos = LEAN ? uni32(its.inj_pos) : its.inj_pos;   // lean: wave-uniform
+    uint32_t ep = LEAN ? uni32(its.epoch) : 0u;  // lean: compact-cell send steps are offsets from ep
     const uint32_t inj_off = gp(P.inj_off)[item], inj_cnt = gp(P.inj_cnt)[item];
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
@@ -424,6 +425,43 @@ void brc_step(const Params* __restrict__ pp) {
     };
     // cell (k, lane) at [k * CW * 64] (CONN send rings: ECHO at + 64, + 128, READY at + 192, + 256)
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
+    // lean kernels: compact u32 cells (brc_internal.h C32_*), row k at [k * 64]
+    const gptr_t<uint32_t> ccells = gp((uint32_t*)P.cells) + item * (uint64_t)(NK + 1) * 64;
+    // lean: this lane's own key slots (bit s mod Q) whose generation wrapped to 0 mod 8 at an
+    // allocation; the wave rewrites those rows fresh (flush_clears) before anything reads them
+    uint32_t clr = 0;
+    auto flush_clears = [&]() {
+        if constexpr (LEAN) {
+            for (uint64_t b = __ballot(clr != 0); b; b &= b - 1) {
+                const int L = __ffsll((unsigned long long)b) - 1;
+                for (uint32_t cm = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr, L)); cm; cm &= cm - 1) {
+                    const uint32_t k = ((uint32_t)L * NV) * Q + (uint32_t)__ffs(cm) - 1u;
+                    (ccells + (size_t)k * 64)[lane] = C32_FRESH;
+                }
+            }
+            clr = 0;
+        }
+    };
+    // lean: move the epoch to t - C32_KEEP when t is too far past it for a 7-bit offset.  Sends
+    // before the new epoch are more than DM steps old and can no longer arrive: they become
+    // C32_OLD (still "sent").  Only rows of slots holding a key, in their current generation.
+    auto rebase = [&]() {
+        if constexpr (LEAN) {
+            const uint32_t nep = t - C32_KEEP, delta = nep - ep;
+            for (uint32_t k = 0; k < NK; ++k) {
+                if (m_s1(uni64(s_meta[k])) == 0) continue;
+                const uint32_t g3 = uni32(s_gen[k]) & C32_GEN;
+                const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
+                uint32_t c = *p;
+                if (((c >> C32_GEN_SH) & C32_GEN) != g3) continue;
+                uint32_t oE = (c >> C32_OE_SH) & 127u, oR = c >> C32_OR_SH;
+                if (oE < C32_OLD) oE = oE >= delta ? oE - delta : C32_OLD;
+                if (oR < C32_OLD) oR = oR >= delta ? oR - delta : C32_OLD;
+                *p = (c & ((1u << C32_OE_SH) - 1u)) | (oE << C32_OE_SH) | (oR << C32_OR_SH);
+            }
+            ep = nep;
+        }
+    };
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     uint64_t c0 = 0, c1 = 0;
@@ -476,7 +514,9 @@ void brc_step(const Params* __restrict__ pp) {
         const uint64_t m = s_meta[mbase + k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
-        s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
+        const uint32_t ng = ((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK;
+        s_gen[mbase + k] = (uint16_t)ng;
+        if (LEAN && (ng & C32_GEN) == 0) clr |= 1u << (s & Qm);   // the compact tag wraps: fresh row
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
@@ -587,6 +627,7 @@ void brc_step(const Params* __restrict__ pp) {
                 send_key(0, v & 3);
                 if constexpr (SPEC) spec_advance();                   // phase 0 may be buffered
             }
+            flush_clears();
         }
         while (inj_pos < inj_cnt) {
             const InjDev r = load_inj(P.inj + inj_off + inj_pos);
@@ -617,6 +658,7 @@ void brc_step(const Params* __restrict__ pp) {
                 const uint32_t os = wave_or(myset);
                 if (mine) {
                     const uint32_t k = r.slot;
+                    bool wrap = false;                   // lean: the compact tag wraps (fresh row)
                     if (d == 0) {
                         uint64_t m = s_meta[mbase + k];
                         uint32_t gen = s_gen[mbase + k] & GEN_MASK;
@@ -626,7 +668,7 @@ void brc_step(const Params* __restrict__ pp) {
                         } else {
                             uint32_t tq = m_tquiet(m);
                             // a declared key holds its slot at least until the next step
-                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; }
+                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; wrap = (gen & C32_GEN) == 0; }
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[mbase + k] = m;
@@ -641,6 +683,9 @@ void brc_step(const Params* __restrict__ pp) {
                             }
                         }
                     }
+                    if constexpr (LEAN) {
+                        if (__ballot(wrap)) (ccells + (size_t)k * 64)[lane] = C32_FRESH;
+                    }
                     q_until = max(q_until, t + hibit(os));
                 }
             } else if (r.kind == BRC_INJ_MSG) {
@@ -650,6 +695,19 @@ void brc_step(const Params* __restrict__ pp) {
                     const uint64_t m = s_meta[mbase + k];
                     if (m_s1(m) != r.s + 1u) {
                         badinj = true;
+                    } else if constexpr (LEAN) {
+                        // compact cell: "sent" = a send-step offset other than C32_NEVER
+                        const uint32_t g3 = s_gen[mbase + k] & C32_GEN;
+                        const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
+                        uint32_t wv = *p;
+                        if (((wv >> C32_GEN_SH) & C32_GEN) != g3) wv = C32_FRESH | (g3 << C32_GEN_SH);
+                        const uint32_t sh = (r.type == BRC_ECHO) ? C32_OE_SH : C32_OR_SH;
+                        if (((wv >> sh) & 127u) == C32_NEVER) {
+                            sent = true;
+                            *p = (wv & ~(127u << sh)) | ((t - ep) << sh);
+                            st_msgs += n;
+                            log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                        }
                     } else {
                         const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
                         uint64_t wv = mycells[(size_t)k * (CW * 64)];
@@ -698,6 +756,7 @@ void brc_step(const Params* __restrict__ pp) {
                     }
                 }
             }
+            flush_clears();                          // PROPOSE / DELIVER may have started a key
         }
         its.initialized = 1;
         return mine_any;
@@ -737,6 +796,7 @@ void brc_step(const Params* __restrict__ pp) {
         if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
         t = LEAN ? uni32(next) : next;
         const uint32_t row = t & (RS - 1);
+        if (LEAN && t - ep > C32_REBASE) rebase();
 
         // ================= BRB: the step's active key slots; one (receiver, key) cell per lane.
         // The ring row becomes a key list (marks made now land on other rows, so it is fixed);
@@ -766,20 +826,21 @@ void brc_step(const Params* __restrict__ pp) {
         // cell word.  Same transitions as process() below, with the per-key work cut down:
         // arrivals are matched against precomputed t - delay, the delay masks are registers
         // (NLR), and only lanes whose cell changes store (exec-masked).
-        const uint32_t tm0 = t - dly0, tm1 = ndl > 1 ? t - dly1 : 0x10000u;   // 0x10000: no 16-bit step
-        const gptr_t<uint64_t> icells = gp(P.cells) + item * (uint64_t)(NK + 1) * 64;   // this item's cells
-        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint64_t wd, uint64_t& nw,
+        // send steps are offsets from the epoch: ts = t - ep <= C32_REBASE, and t - delay - ep
+        // wraps to a huge value (matching no 7-bit offset) for a delay reaching before the epoch
+        const uint32_t ts = t - ep;
+        const uint32_t tm0 = ts - dly0, tm1 = ndl > 1 ? ts - dly1 : 0x10000u;   // 0x10000: no 7-bit offset
+        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint32_t wd, uint32_t& nw,
                                 bool& wr) {
-            const uint32_t gen = gw & GEN_MASK;
+            const uint32_t g3 = gw & C32_GEN;
             if (m_s1(m) == 0) return;                            // the slot holds no key
             ++nk_lean;                                           // lane loads: one word per real lane
             BRC_KCOUNT(0);
-            const uint32_t wlo = (uint32_t)wd, whi = (uint32_t)(wd >> 32);
             // a stale word (older generation) is a fresh cell: lanes that are not real replicas
             // and Byzantine lanes never store here, so their words read "never sent"
-            const bool cur = (wlo >> 19) == gen;                 // gen: bits 19..31
-            const uint32_t lo = cur ? wlo : 0u, hi = cur ? whi : 0xFFFFFFFFu;
-            const uint32_t tE = hi & 0xFFFF, tR = hi >> 16;      // steps this lane SENT ECHO / READY
+            const bool cur = ((wd >> C32_GEN_SH) & C32_GEN) == g3;
+            const uint32_t lo = cur ? wd : C32_FRESH;
+            const uint32_t tE = (lo >> C32_OE_SH) & 127u, tR = lo >> C32_OR_SH;   // offsets: SENT ECHO / READY
             // arrivals: senders whose message lands now, per delay present (empty ballots skipped)
             uint32_t ea = 0, ra = 0;
             uint64_t be_any = 0, br_any = 0;
@@ -795,7 +856,7 @@ void brc_step(const Params* __restrict__ pp) {
                 ra = popc(br1 ^ ((br0 ^ br1) & RL0));
                 be_any = be0 | be1; br_any = br0 | br1;
             } else {
-                const uint32_t dE = t - tE, dR = t - tR;
+                const uint32_t dE = ts - tE, dR = ts - tR;      // C32_OLD / C32_NEVER: no delay
                 Unrolled<DM>::run([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     if ((uint32_t)j < ndl) {
@@ -837,7 +898,9 @@ void brc_step(const Params* __restrict__ pp) {
             const bool opn = has && !(lo & F_DEL);
             if (!__ballot(opn)) { BRC_KCOUNT(2); return; }
             BRC_KCOUNT(3);
-            uint32_t fl = lo & 31, ec = (lo >> 5) & 127, rc = (lo >> 12) & 127;
+            // F_ES / F_RS are "has a send step"
+            uint32_t fl = (lo & 7u) | (tE != C32_NEVER ? F_ES : 0u) | (tR != C32_NEVER ? F_RS : 0u);
+            uint32_t ec = (lo >> 3) & 63u, rc = (lo >> 9) & 63u;
             uint32_t es = 0, rs = 0, dl = 0;                     // 0/1: ECHO sent, READY sent, delivered
             const uint32_t sa = (opn && s_arr) ? 1u : 0u;
             const uint32_t e = opn ? ea : 0u, r = opn ? ra : 0u;
@@ -884,10 +947,11 @@ void brc_step(const Params* __restrict__ pp) {
                     rs |= r2;
                 }
             }
-            {   // new word for open cells; the others keep theirs
-                const uint32_t nlo = fl | (ec << 5) | (rc << 12) | (gen << 19);
-                const uint32_t nhi = (es ? t : tE) | ((rs ? t : tR) << 16);
-                nw = (uint64_t)nlo | ((uint64_t)nhi << 32);
+            {   // new word for open cells; the others keep theirs.  A count reaches 64 only when
+                // every sender's message of that type has arrived, so none is compared again: the
+                // stored counts saturate at 63 without changing any later transition
+                nw = (fl & 7u) | (min(ec, 63u) << 3) | (min(rc, 63u) << 9) | (g3 << C32_GEN_SH) |
+                     ((es ? ts : tE) << C32_OE_SH) | ((rs ? ts : tR) << C32_OR_SH);
                 wr = opn;
                 st_bcast += es + rs;
             }
@@ -1051,7 +1115,7 @@ void brc_step(const Params* __restrict__ pp) {
             }
         };
         // lean key pipeline registers; declared here so they stay live to the end of the step (below)
-        uint64_t w[CHUNK];
+        uint32_t w[CHUNK];                   // lean: compact cell words in flight
         uint32_t kk[CHUNK];
         if constexpr (LEAN) {
             // software pipeline, unrolled by CHUNK so the in-flight cell words never move between
@@ -1060,7 +1124,7 @@ void brc_step(const Params* __restrict__ pp) {
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
-            auto cell = [&](uint32_t k) { return (icells + (size_t)k * 64)[lane]; };
+            auto cell = [&](uint32_t k) { return (ccells + (size_t)k * 64)[lane]; };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
             Unrolled<CHUNK>::run([&](auto ci) {
@@ -1087,13 +1151,13 @@ void brc_step(const Params* __restrict__ pp) {
                     // slots past the list write the trash row): with a fixed count of memory
                     // operations between a load and its use, the compiler waits for exactly that
                     // load (vmcnt(CHUNK - 1)) instead of for the younger stores as well
-                    uint64_t nw = w[c];
+                    uint32_t nw = w[c];
                     bool wr = false;
                     if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c], nw, wr);
 #ifdef BRC_WHOLE_STORE
-                    (icells + (size_t)kk[c] * 64)[lane] = wr ? nw : w[c];
+                    (ccells + (size_t)kk[c] * 64)[lane] = wr ? nw : w[c];
 #else
-                    if (wr) (icells + (size_t)kk[c] * 64)[lane] = nw;
+                    if (wr) (ccells + (size_t)kk[c] * 64)[lane] = nw;
 #endif
                     kk[c] = (uint32_t)(uni64(knext) >> (16 * c)) & 0xFFFFu;
                     w[c] = cell(kk[c]);
@@ -1155,6 +1219,7 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
         }
+        flush_clears();                                  // keys the consensus started this step
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(2);
 
@@ -1209,7 +1274,7 @@ void brc_step(const Params* __restrict__ pp) {
     }
     if (lane == 0) {
         gp(P.actany)[item] = any_rows;
-        ItemState o = {t, inj_pos, 1u, 0u};
+        ItemState o = {t, inj_pos, 1u, ep};
         P.items[item] = o;
     }
     if (honest && P.protocol == BRC_PROTO_CONSENSUS) {

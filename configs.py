@@ -61,7 +61,10 @@ def workloads(L):
     return W
 
 
-FLOOR_BYTES_PER_CELL_STEP = 16      # the cell word read + written (one u64 per (receiver, key))
+def cell_bytes(n, peer_mode=0):
+    """Bytes of one (receiver, key) cell: 4 on the lean kernels (33 <= n <= 64, sender peers:
+    brc_internal.h C32_*), 8 on the others."""
+    return 4 if 32 < n <= 64 and peer_mode == 0 else 8
 
 
 def measured_traffic(name, kernel_ms):
@@ -83,18 +86,19 @@ def measured_traffic(name, kernel_ms):
     return best
 
 
-def roofline(name, n, bpc, cell_steps, kernel_ms):
-    """Algorithmic, floor (this layout's 16 B per cell-step) and counter-measured
-    HBM fractions of the dominant kernel, as bench.py reports them."""
+def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0):
+    """Algorithmic, floor (this layout's cell word read + written per cell-step)
+    and counter-measured HBM fractions of the dominant kernel, as bench.py reports them."""
     sec = kernel_ms / 1e3
+    floor_b = 2 * cell_bytes(n, peer_mode)
     achieved = bpc * cell_steps / sec / 1e9
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": achieved,
            "frac": achieved / HBM_PEAK_GBS,
-           "floor_frac": FLOOR_BYTES_PER_CELL_STEP * cell_steps / sec / 1e9 / HBM_PEAK_GBS,
+           "floor_frac": floor_b * cell_steps / sec / 1e9 / HBM_PEAK_GBS, "cell_bytes": floor_b // 2,
            "traffic": None, "traffic_frac": None,
            "note": "algorithmic %d B per cell-step (SURVEY 8(d) at n=%d) credits n-bit sets this layout never "
                    "moves, so frac can pass 1; floor_frac: %d B per cell-step; traffic_frac: rocprofv3 "
-                   "FETCH_SIZE x 2 + WRITE_SIZE" % (bpc, n, FLOOR_BYTES_PER_CELL_STEP)}
+                   "FETCH_SIZE x 2 + WRITE_SIZE" % (bpc, n, floor_b)}
     t = measured_traffic(name, kernel_ms)
     if t:
         out["traffic"], out["traffic_source"] = t
@@ -164,7 +168,7 @@ def main():
                 "statuses": {k: st[k] for k in ("done", "quiescent", "stepcap", "overflow", "running")},
                 "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
                 "cell_steps_per_launch": st["cell_steps"], "lane_loads_per_launch": st["lane_loads"],
-                "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms),
+                "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms, kw.get("peer_mode", 0)),
             }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

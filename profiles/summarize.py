@@ -9,8 +9,9 @@ profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
 
 HBM bytes follow MI355X_MICROARCH.md (rocprofv3 / HBM section): FETCH_SIZE and WRITE_SIZE are
 in KiB and come from separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of a
-coalesced streaming read, so it is doubled.  The kernel's loads are 8 B/lane coalesced
-512-B wave accesses, where the doubling was checked against SQ_INSTS_VMEM_RD x 512 B.
+coalesced streaming read, so it is doubled.  The kernel's cell loads are coalesced wave
+accesses of one cell per lane (8 B until r2e, 4 B since), where the doubling is checked against
+SQ_INSTS_VMEM_RD x 64 x cell bytes.
 """
 import csv
 import glob
@@ -63,8 +64,9 @@ def main():
         out.update({"fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
                     "hbm_gbs": (fetch + write) / avg_ns if avg_ns else None})
         if "SQ_INSTS_VMEM_RD" in k:
-            out["vmem_rd_bytes_issued"] = k["SQ_INSTS_VMEM_RD"] * 512.0
-            out["vmem_wr_bytes_issued"] = k.get("SQ_INSTS_VMEM_WR", 0.0) * 512.0
+            wave_bytes = 64.0 * (bench or {}).get("roofline", {}).get("cell_bytes", 8)   # one cell per lane
+            out["vmem_rd_bytes_issued"] = k["SQ_INSTS_VMEM_RD"] * wave_bytes
+            out["vmem_wr_bytes_issued"] = k.get("SQ_INSTS_VMEM_WR", 0.0) * wave_bytes
     if bench and "config" not in bench:             # a configs.py workload line
         out["workload"], out["mode"] = bench.get("workload"), bench.get("mode")
         out["instances"], out["bench_kernel_ms"] = bench.get("instances"), bench.get("kernel_ms")
@@ -75,6 +77,7 @@ def main():
         out["workload"] = cfg.get("workload", "").split(":")[0]
         out["mode"] = cfg.get("mode", "reference")
         out["bench_kernel_ms"] = bench.get("kernel_ms")
+        out["cell_bytes"] = bench.get("roofline", {}).get("cell_bytes", 8)
     # the bench reads profiles/pmc_traffic.json for its headline (reference) leg only
     paths = [os.path.join(dest, "pmc_traffic.json")]
     if out.get("mode", "reference") == "reference" and out.get("headline", True):

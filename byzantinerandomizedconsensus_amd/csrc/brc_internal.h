@@ -60,13 +60,14 @@ struct InjDev {       // 48 B, per item CSR, sorted by t
 struct ItemState { uint32_t t, inj_pos, initialized, epoch; };
 
 // Compact cell of the lean kernels (NPAD = 64, sender peers: brc_step.h), one u32:
-//   bits 0-2 F_EEX, F_REX, F_DEL   bits 3-8 |echo set|   bits 9-14 |ready set| (both saturate at 63)
-//   bits 15-17 slot generation mod 8
-//   bits 18-24 / 25-31: step this lane SENT its ECHO / READY, as an offset from the item's epoch;
+//   bits 0-4 flags F_EEX, F_REX, F_DEL, F_ES, F_RS
+//   bits 5-10 |echo set|, 11-16 |ready set| (both saturate at 63)
+//   bits 17-23 / 24-30: step this lane SENT its ECHO / READY, as an offset from the item's epoch;
 //   C32_OLD = sent more than DM steps before the epoch, C32_NEVER = not sent
-constexpr uint32_t C32_GEN_SH = 15, C32_GEN = 7, C32_OE_SH = 18, C32_OR_SH = 25;
+// No generation tag: a slot's row is rewritten fresh whenever the slot is (re)allocated.
+constexpr uint32_t C32_EC_SH = 5, C32_RC_SH = 11, C32_OE_SH = 17, C32_OR_SH = 24;
 constexpr uint32_t C32_NEVER = 127, C32_OLD = 126;
-constexpr uint32_t C32_FRESH = (C32_NEVER << C32_OE_SH) | (C32_NEVER << C32_OR_SH);   // generation 0
+constexpr uint32_t C32_FRESH = (C32_NEVER << C32_OE_SH) | (C32_NEVER << C32_OR_SH);
 constexpr uint32_t C32_REBASE = 100;   // a step more than this past the epoch moves the epoch first
 constexpr uint32_t C32_KEEP = 17;      // ... to t - C32_KEEP: sends in the last 16 steps keep their step
 

@@ -110,7 +110,9 @@ __device__ __forceinline__ uint32_t m_s1(uint64_t m) { return (uint32_t)(m & 0xF
 __device__ __forceinline__ uint32_t m_tsend(uint64_t m) { return (uint32_t)((m >> 16) & 0xFFFF); }
 __device__ __forceinline__ uint32_t m_tquiet(uint64_t m) { return (uint32_t)((m >> 32) & 0xFFFF); }
 __device__ __forceinline__ uint32_t m_sender(uint64_t m) { return (uint32_t)((m >> 48) & 0xFF); }
-__device__ __forceinline__ uint32_t m_value(uint64_t m) { return (uint32_t)((m >> 56) & 0xFF); }
+__device__ __forceinline__ uint32_t m_value(uint64_t m) { return (uint32_t)((m >> 56) & 0x7F); }
+// lean kernels: the LDS copy of a restricted-SEND key's metadata carries this bit (value ids are < 4)
+constexpr uint64_t M_RESTRICTED = 1ull << 63;
 __device__ __forceinline__ uint64_t m_pack(uint32_t s1, uint32_t tsend, uint32_t tquiet, uint32_t sender, uint32_t value) {
     return (uint64_t)(s1 & 0xFFFF) | ((uint64_t)(tsend & 0xFFFF) << 16) | ((uint64_t)(tquiet & 0xFFFF) << 32) |
            ((uint64_t)(sender & 0xFF) << 48) | ((uint64_t)(value & 0xFF) << 56);
@@ -321,8 +323,9 @@ void brc_step(const Params* __restrict__ pp) {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
             const bool ok = item * IPW + i / NK < P.instances;
-            s_meta[i] = ok ? gp(P.meta)[mb + i] : 0ull;
-            s_gen[i] = ok ? gen16(gp(P.mgen)[mb + i]) : (uint16_t)0;
+            const uint32_t g32 = ok ? gp(P.mgen)[mb + i] : 0u;
+            s_meta[i] = ok ? gp(P.meta)[mb + i] | ((LEAN && (g32 & GEN_RESTRICTED)) ? M_RESTRICTED : 0ull) : 0ull;
+            s_gen[i] = gen16(g32);
         }
         for (uint32_t i = lane; i < RS * nkw; i += 64) s_act[i] = gp(P.act)[item * RS * nkw + i];
         for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
@@ -427,8 +430,8 @@ void brc_step(const Params* __restrict__ pp) {
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
     // lean kernels: compact u32 cells (brc_internal.h C32_*), row k at [k * 64]
     const gptr_t<uint32_t> ccells = gp((uint32_t*)P.cells) + item * (uint64_t)(NK + 1) * 64;
-    // lean: this lane's own key slots (bit s mod Q) whose generation wrapped to 0 mod 8 at an
-    // allocation; the wave rewrites those rows fresh (flush_clears) before anything reads them
+    // lean: this lane's own key slots (bit s mod Q) allocated since the last flush; the wave
+    // rewrites those rows fresh (flush_clears) before anything reads them
     uint32_t clr = 0;
     auto flush_clears = [&]() {
         if constexpr (LEAN) {
@@ -444,16 +447,14 @@ void brc_step(const Params* __restrict__ pp) {
     };
     // lean: move the epoch to t - C32_KEEP when t is too far past it for a 7-bit offset.  Sends
     // before the new epoch are more than DM steps old and can no longer arrive: they become
-    // C32_OLD (still "sent").  Only rows of slots holding a key, in their current generation.
+    // C32_OLD (still "sent").  Only rows of slots holding a key.
     auto rebase = [&]() {
         if constexpr (LEAN) {
             const uint32_t nep = t - C32_KEEP, delta = nep - ep;
             for (uint32_t k = 0; k < NK; ++k) {
                 if (m_s1(uni64(s_meta[k])) == 0) continue;
-                const uint32_t g3 = uni32(s_gen[k]) & C32_GEN;
                 const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
-                uint32_t c = *p;
-                if (((c >> C32_GEN_SH) & C32_GEN) != g3) continue;
+                const uint32_t c = *p;
                 uint32_t oE = (c >> C32_OE_SH) & 127u, oR = c >> C32_OR_SH;
                 if (oE < C32_OLD) oE = oE >= delta ? oE - delta : C32_OLD;
                 if (oR < C32_OLD) oR = oR >= delta ? oR - delta : C32_OLD;
@@ -485,7 +486,8 @@ void brc_step(const Params* __restrict__ pp) {
 
     uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
     uint32_t st_bcast = 0;                       // lean path: ECHO/READY broadcasts (n messages each)
-    uint32_t nk_lean = 0;                        // lean path: keys processed (wave-uniform)
+    // lean path, wave-uniform: key list entries (nk_lean) minus empty slots among them (nk_skip)
+    uint32_t nk_lean = 0, nk_skip = 0;
 
     auto log_ev = [&](uint32_t kind, uint32_t node, uint32_t type, uint32_t a, uint32_t b, uint32_t v) {
         if (EV) {
@@ -514,9 +516,8 @@ void brc_step(const Params* __restrict__ pp) {
         const uint64_t m = s_meta[mbase + k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
-        const uint32_t ng = ((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK;
-        s_gen[mbase + k] = (uint16_t)ng;
-        if (LEAN && (ng & C32_GEN) == 0) clr |= 1u << (s & Qm);   // the compact tag wraps: fresh row
+        s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
+        if (LEAN) clr |= 1u << (s & Qm);                 // compact cells: the row is rewritten fresh
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
@@ -658,7 +659,7 @@ void brc_step(const Params* __restrict__ pp) {
                 const uint32_t os = wave_or(myset);
                 if (mine) {
                     const uint32_t k = r.slot;
-                    bool wrap = false;                   // lean: the compact tag wraps (fresh row)
+                    bool fresh = false;                  // lean: the slot is (re)allocated: fresh row
                     if (d == 0) {
                         uint64_t m = s_meta[mbase + k];
                         uint32_t gen = s_gen[mbase + k] & GEN_MASK;
@@ -668,12 +669,13 @@ void brc_step(const Params* __restrict__ pp) {
                         } else {
                             uint32_t tq = m_tquiet(m);
                             // a declared key holds its slot at least until the next step
-                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; wrap = (gen & C32_GEN) == 0; }
+                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; fresh = true; }
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[mbase + k] = m;
                             const bool restricted = is_send && (r.dst & all64) != all64;
                             s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
+                            if (LEAN && restricted) s_meta[mbase + k] = m | M_RESTRICTED;
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 gp(P.kdst)[inst * NK + k] = r.dst;
@@ -684,7 +686,7 @@ void brc_step(const Params* __restrict__ pp) {
                         }
                     }
                     if constexpr (LEAN) {
-                        if (__ballot(wrap)) (ccells + (size_t)k * 64)[lane] = C32_FRESH;
+                        if (__ballot(fresh)) (ccells + (size_t)k * 64)[lane] = C32_FRESH;
                     }
                     q_until = max(q_until, t + hibit(os));
                 }
@@ -696,15 +698,14 @@ void brc_step(const Params* __restrict__ pp) {
                     if (m_s1(m) != r.s + 1u) {
                         badinj = true;
                     } else if constexpr (LEAN) {
-                        // compact cell: "sent" = a send-step offset other than C32_NEVER
-                        const uint32_t g3 = s_gen[mbase + k] & C32_GEN;
+                        // compact cell: F_ES / F_RS and the send-step offset
                         const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
-                        uint32_t wv = *p;
-                        if (((wv >> C32_GEN_SH) & C32_GEN) != g3) wv = C32_FRESH | (g3 << C32_GEN_SH);
+                        const uint32_t wv = *p;
+                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
                         const uint32_t sh = (r.type == BRC_ECHO) ? C32_OE_SH : C32_OR_SH;
-                        if (((wv >> sh) & 127u) == C32_NEVER) {
+                        if (!(wv & bit)) {
                             sent = true;
-                            *p = (wv & ~(127u << sh)) | ((t - ep) << sh);
+                            *p = ((wv | bit) & ~(127u << sh)) | ((t - ep) << sh);
                             st_msgs += n;
                             log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                         }
@@ -811,6 +812,7 @@ void brc_step(const Params* __restrict__ pp) {
             nkeys += (uint32_t)__popcll(bits);
         }
         if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
+        if constexpr (LEAN) nk_lean += nkeys;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(0);
         // p < nkeys + CHUNK: padded list.  The key ids stay in SGPRs with the words they address,
@@ -830,16 +832,11 @@ void brc_step(const Params* __restrict__ pp) {
         // wraps to a huge value (matching no 7-bit offset) for a delay reaching before the epoch
         const uint32_t ts = t - ep;
         const uint32_t tm0 = ts - dly0, tm1 = ndl > 1 ? ts - dly1 : 0x10000u;   // 0x10000: no 7-bit offset
-        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t gw, const uint32_t wd, uint32_t& nw,
-                                bool& wr) {
-            const uint32_t g3 = gw & C32_GEN;
-            if (m_s1(m) == 0) return;                            // the slot holds no key
-            ++nk_lean;                                           // lane loads: one word per real lane
+        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t lo, uint32_t& nw, bool& wr) {
+            if (m_s1(m) == 0) { ++nk_skip; return; }            // the slot holds no key
             BRC_KCOUNT(0);
-            // a stale word (older generation) is a fresh cell: lanes that are not real replicas
-            // and Byzantine lanes never store here, so their words read "never sent"
-            const bool cur = ((wd >> C32_GEN_SH) & C32_GEN) == g3;
-            const uint32_t lo = cur ? wd : C32_FRESH;
+            // lanes that are not real replicas and Byzantine lanes never update their cells here, so
+            // their words keep the fresh row's "never sent" unless an injection sent for them
             const uint32_t tE = (lo >> C32_OE_SH) & 127u, tR = lo >> C32_OR_SH;   // offsets: SENT ECHO / READY
             // arrivals: senders whose message lands now, per delay present (empty ballots skipped)
             uint32_t ea = 0, ra = 0;
@@ -885,7 +882,7 @@ void brc_step(const Params* __restrict__ pp) {
             }
             if (s_win) {
                 bool hit = (Lmask(sj) >> m_sender(m)) & 1;
-                if (gw & GEN16_RESTRICTED) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
+                if (m & M_RESTRICTED) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = honest && hit;
             }
             const bool has = honest && (s_arr || ea || ra);
@@ -898,9 +895,7 @@ void brc_step(const Params* __restrict__ pp) {
             const bool opn = has && !(lo & F_DEL);
             if (!__ballot(opn)) { BRC_KCOUNT(2); return; }
             BRC_KCOUNT(3);
-            // F_ES / F_RS are "has a send step"
-            uint32_t fl = (lo & 7u) | (tE != C32_NEVER ? F_ES : 0u) | (tR != C32_NEVER ? F_RS : 0u);
-            uint32_t ec = (lo >> 3) & 63u, rc = (lo >> 9) & 63u;
+            uint32_t fl = lo & 31u, ec = (lo >> C32_EC_SH) & 63u, rc = (lo >> C32_RC_SH) & 63u;
             uint32_t es = 0, rs = 0, dl = 0;                     // 0/1: ECHO sent, READY sent, delivered
             const uint32_t sa = (opn && s_arr) ? 1u : 0u;
             const uint32_t e = opn ? ea : 0u, r = opn ? ra : 0u;
@@ -950,7 +945,7 @@ void brc_step(const Params* __restrict__ pp) {
             {   // new word for open cells; the others keep theirs.  A count reaches 64 only when
                 // every sender's message of that type has arrived, so none is compared again: the
                 // stored counts saturate at 63 without changing any later transition
-                nw = (fl & 7u) | (min(ec, 63u) << 3) | (min(rc, 63u) << 9) | (g3 << C32_GEN_SH) |
+                nw = fl | (min(ec, 63u) << C32_EC_SH) | (min(rc, 63u) << C32_RC_SH) |
                      ((es ? ts : tE) << C32_OE_SH) | ((rs ? ts : tR) << C32_OR_SH);
                 wr = opn;
                 st_bcast += es + rs;
@@ -1135,11 +1130,9 @@ void brc_step(const Params* __restrict__ pp) {
             });
             for (uint32_t p = 0; p < nkeys; p += CHUNK) {
                 uint64_t mm[CHUNK];
-                uint32_t gg[CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     mm[c] = s_meta[kk[c]];
-                    gg[c] = s_gen[kk[c]];
                 });
                 // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
                 // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own
@@ -1153,7 +1146,7 @@ void brc_step(const Params* __restrict__ pp) {
                     // load (vmcnt(CHUNK - 1)) instead of for the younger stores as well
                     uint32_t nw = w[c];
                     bool wr = false;
-                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), uni32(gg[c]), w[c], nw, wr);
+                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), w[c], nw, wr);
 #ifdef BRC_WHOLE_STORE
                     (ccells + (size_t)kk[c] * 64)[lane] = wr ? nw : w[c];
 #else
@@ -1268,7 +1261,7 @@ void brc_step(const Params* __restrict__ pp) {
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i]; gp(P.mgen)[mb + i] = gen32(s_gen[i]); }
+            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i] & ~M_RESTRICTED; gp(P.mgen)[mb + i] = gen32(s_gen[i]); }
         }
         for (uint32_t i = lane; i < RS * nkw; i += 64) gp(P.act)[item * RS * nkw + i] = s_act[i];
     }
@@ -1294,7 +1287,7 @@ void brc_step(const Params* __restrict__ pp) {
         }
     }
     st_msgs += st_bcast * n;
-    if (LEAN && real) st_loads += nk_lean;
+    if (LEAN && real) st_loads += nk_lean - nk_skip;
     // statistics: reduce over the segment, its leader writes the instance row
     uint32_t sums[4] = {st_msgs, st_arr, st_cells, st_del};
 #pragma unroll

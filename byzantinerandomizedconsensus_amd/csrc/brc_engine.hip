@@ -376,7 +376,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xw,
                                             spec, c.key_window)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
-                                                c.variants, e->rs) * WPB;
+                                                c.variants, e->rs, e->compact) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";

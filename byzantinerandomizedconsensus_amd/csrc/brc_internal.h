@@ -108,17 +108,18 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
-// mgen[IPW*NK] u16 | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
+// mgen[IPW*NK] u16 (not on the lean kernels) | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
 // reused as the consensus snapshot snap[IPW*NK] u16)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
-                                                       uint32_t Q, uint32_t nv, uint32_t rs) {
+                                                       uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // the key-list area doubles as the consensus phase's snapshot of every slot's (value, s + 1)
     const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
-    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + (ipw * NK + 3) / 4 + (klist_u16 + 3) / 4);
+    const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
+    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

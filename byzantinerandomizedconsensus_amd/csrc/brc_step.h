@@ -290,7 +290,7 @@ void brc_step(const Params* __restrict__ pp) {
     const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
     const bool seen_on = NV > 1;                 // SPEC: host sets needed only with key variants
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
-    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV, RS) / 8);
+    uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV, RS, LEAN) / 8);
     uint64_t* s_act = s_meta + IPW * NK;
     uint64_t* s_dbits = s_act + RS * nkw;        // this step's deliveries, per lane
     T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
@@ -298,8 +298,9 @@ void brc_step(const Params* __restrict__ pp) {
     // SPEC: s_cnt[q*64 + lane] = #origins | #"0" << 10 | #"1" << 20 for phase slot q
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));
     T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
-    uint16_t* s_gen = (uint16_t*)(s_dbits + 64 * nkw + h_words + l_words);   // gen | GEN16_RESTRICTED
-    uint16_t* s_klist = s_gen + ((IPW * NK + 3) & ~3u);                      // this step's active key slots
+    // gen | GEN16_RESTRICTED (lean kernels keep no generations: no area)
+    uint16_t* s_gen = (uint16_t*)(s_dbits + 64 * nkw + h_words + l_words);
+    uint16_t* s_klist = s_gen + (LEAN ? 0u : ((IPW * NK + 3) & ~3u));        // this step's active key slots
     // consensus phase: the key list is dead, and its area holds snap[IPW*NK] = value << 14 | (s + 1) of
     // every slot as the BRB phase left it.  A replica's phase change reallocates its own slot
     // mid-loop (send_key), while another replica may still have to count a delivery of the old key
@@ -325,7 +326,7 @@ void brc_step(const Params* __restrict__ pp) {
             const bool ok = item * IPW + i / NK < P.instances;
             const uint32_t g32 = ok ? gp(P.mgen)[mb + i] : 0u;
             s_meta[i] = ok ? gp(P.meta)[mb + i] | ((LEAN && (g32 & GEN_RESTRICTED)) ? M_RESTRICTED : 0ull) : 0ull;
-            s_gen[i] = gen16(g32);
+            if (!LEAN) s_gen[i] = gen16(g32);
         }
         for (uint32_t i = lane; i < RS * nkw; i += 64) s_act[i] = gp(P.act)[item * RS * nkw + i];
         for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
@@ -516,7 +517,7 @@ void brc_step(const Params* __restrict__ pp) {
         const uint64_t m = s_meta[mbase + k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
-        s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
+        if (!LEAN) s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
         if (LEAN) clr |= 1u << (s & Qm);                 // compact cells: the row is rewritten fresh
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
@@ -662,7 +663,7 @@ void brc_step(const Params* __restrict__ pp) {
                     bool fresh = false;                  // lean: the slot is (re)allocated: fresh row
                     if (d == 0) {
                         uint64_t m = s_meta[mbase + k];
-                        uint32_t gen = s_gen[mbase + k] & GEN_MASK;
+                        uint32_t gen = LEAN ? 0u : s_gen[mbase + k] & GEN_MASK;
                         const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
                         if ((!declared && m_s1(m) != 0 && t < m_tquiet(m)) || r.s >= P.s_limit) {
                             ovf = true;
@@ -674,7 +675,7 @@ void brc_step(const Params* __restrict__ pp) {
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[mbase + k] = m;
                             const bool restricted = is_send && (r.dst & all64) != all64;
-                            s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
+                            if (!LEAN) s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
                             if (LEAN && restricted) s_meta[mbase + k] = m | M_RESTRICTED;
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
@@ -1261,7 +1262,10 @@ void brc_step(const Params* __restrict__ pp) {
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            if (item * IPW + i / NK < P.instances) { gp(P.meta)[mb + i] = s_meta[i] & ~M_RESTRICTED; gp(P.mgen)[mb + i] = gen32(s_gen[i]); }
+            if (item * IPW + i / NK < P.instances) {
+                gp(P.meta)[mb + i] = s_meta[i] & ~M_RESTRICTED;
+                gp(P.mgen)[mb + i] = LEAN ? ((s_meta[i] & M_RESTRICTED) ? GEN_RESTRICTED : 0u) : gen32(s_gen[i]);
+            }
         }
         for (uint32_t i = lane; i < RS * nkw; i += 64) gp(P.act)[item * RS * nkw + i] = s_act[i];
     }

@@ -51,7 +51,7 @@ def workloads(L):
                                            byzantine=list(range(11, 16)), mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
         "cfg4-ref": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                          round_cap=1, key_window=4)),
-        "cfg4-spec": (1 << 19, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+        "cfg4-spec": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                           round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
     }
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
@@ -111,6 +111,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--instances", type=int, default=0, help="override the workloads' instance counts")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -137,6 +138,7 @@ def main():
     names = [x for x in args.only.split(",") if x] or list(W)
     for name in names:
         size, per_gpu, kw = W[name]
+        size = args.instances or size
         first, count = shard.shard_range(size * world if per_gpu else size, world, rank)
         n = kw["n"]
         bpc = 6 * ((n + 7) // 8) + 2

@@ -5,8 +5,8 @@ from oracle import oracle
 from tests import golden_io
 
 GROUPS = golden_io.groups()
-CASES = [(g, i) for g, cases in GROUPS.items() for i in range(len(cases))
-         if g != "cons_slowset_n64"]
+LARGE = ("cons_slowset_n64", "cons_slowset_n256")      # ~10 s / ~30 s oracle runs: tests of their own
+CASES = [(g, i) for g, cases in GROUPS.items() for i in range(len(cases)) if g not in LARGE]
 
 
 @pytest.mark.parametrize("group,idx", CASES, ids=["%s-%d" % c for c in CASES])
@@ -17,10 +17,13 @@ def test_oracle_matches_reference(group, idx):
 
 
 @pytest.mark.slow
-def test_oracle_matches_reference_n64():
-    case = GROUPS["cons_slowset_n64"][0]
+@pytest.mark.parametrize("group", LARGE)
+def test_oracle_matches_reference_large(group):
+    """n = 64 and n = 256 (SURVEY §8(d) cfg4 / cfg5 committees): reference-protocol consensus to the
+    first decision under slow-set delays, generated from the unmodified reference."""
+    case = GROUPS[group][0]
     got = oracle.run(case["spec"])
-    golden_io.assert_matches(case["result"], got, "cons_slowset_n64")
+    golden_io.assert_matches(case["result"], got, group)
 
 
 def test_fixture_inventory():

@@ -46,6 +46,7 @@ def canonical(result):
 
 
 def compact(result):
+    raw = result["events"]
     result = canonical(result)
     ev = result["events"]
     out = {k: result[k] for k in ("status", "t_stop", "msgs_sent", "arrivals")}
@@ -53,6 +54,10 @@ def compact(result):
     out["digest"] = {k: digest(v) for k, v in ev.items()}
     total = sum(len(v) for v in ev.values())
     out["events"] = ev if total <= FULL_EVENT_LIMIT else {"decide": ev["decide"]}
+    # the upcalls in the order the reference issued them (each kind on its own), for small runs:
+    # pins the per-step order the class API replays, not only the canonical sort
+    if total <= FULL_EVENT_LIMIT:
+        out["raw_order"] = {k: [list(r) for r in raw[k]] for k in ("deliver", "decide")}
     return out
 
 

@@ -26,6 +26,24 @@ def test_oracle_matches_reference_large(group):
     golden_io.assert_matches(case["result"], got, group)
 
 
+RAW = [(g, i) for g, cases in GROUPS.items() for i, c in enumerate(cases) if "raw_order" in c["result"]]
+
+
+@pytest.mark.parametrize("group,idx", RAW, ids=["%s-%d" % c for c in RAW])
+def test_oracle_upcall_order_is_the_references(group, idx):
+    """Not only the canonical sort: the oracle issues deliver / decide upcalls in the order the
+    reference issued them (the fixture's raw_order, recorded by the harness as they happened)."""
+    case = GROUPS[group][idx]
+    got = oracle.run(case["spec"])
+    for k in ("deliver", "decide"):
+        assert [list(r) for r in got["events"][k]] == case["result"]["raw_order"][k], "%s[%d] %s" % (group, idx, k)
+
+
+def test_raw_order_fixtures_present():
+    assert {g for g, _ in RAW} >= {"brb_uniform_n10", "conn_brb_uniform_n10", "cons_brc_test_n6",
+                                   "conn_cons_brc_test_n6", "cons_uniform_n6"}
+
+
 def test_fixture_inventory():
     # every SURVEY §4 known-answer scenario has a fixture
     names = {c["spec"]["name"] for c in GROUPS["kat"]}

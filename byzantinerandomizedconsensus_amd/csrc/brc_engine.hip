@@ -164,6 +164,7 @@ struct Engine {
     uint64_t* byz = nullptr; int8_t* prop = nullptr;
     brc_event* events = nullptr; unsigned long long* event_count = nullptr;
     unsigned long long* gcount = nullptr;
+    uint64_t* dbits = nullptr;                   // lean SPEC: per-wave delivery bitmaps (brc_step.h DBG)
     Params* dparams = nullptr;                   // device copy of the launch parameters
     Params hparams;
     std::vector<std::vector<InjDev>> pending;   // per item: uploaded-but-unconsumed + new
@@ -216,7 +217,7 @@ static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks,
 static void free_all(Engine* e) {
     void* ps[] = {e->cells, e->meta, e->mgen, e->kdst, e->act, e->actany, e->items, e->inst, e->istats,
                   e->cons0, e->cons1, e->hmask, e->inj, e->inj_off, e->inj_cnt, e->byz, e->prop, e->events,
-                  e->event_count, e->gcount, e->dparams};
+                  e->event_count, e->gcount, e->dbits, e->dparams};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -402,6 +403,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {&e->hmask, (size_t)e->nitems * e->cons_bytes}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
+        {(void**)&e->dbits, (e->compact && spec) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
     };
     for (auto& a : allocs)
         if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) {
@@ -578,7 +580,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
-    P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount;
+    P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount; P.dbits = e->dbits;
     const uint32_t blocks = e->wide ? (uint32_t)e->nitems : (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));

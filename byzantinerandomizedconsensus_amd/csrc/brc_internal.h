@@ -90,6 +90,7 @@ struct Params {
     const InjDev* inj; const uint32_t* inj_off; const uint32_t* inj_cnt;
     const uint64_t* byz; const int8_t* prop;
     brc_event* events; unsigned long long* event_count;
+    uint64_t* dbits;              // lean SPEC: per-wave delivery bitmaps [item][nkw][64] (brc_step.h DBG)
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
                                   // [6] instances still running after the launch
 };
@@ -107,7 +108,7 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 }
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
-// meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 | consensus area | L[nL][64] T |
+// meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u16 (not on the lean kernels) | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
 // reused as the consensus snapshot snap[IPW*NK] u16)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
@@ -119,7 +120,8 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     // the key-list area doubles as the consensus phase's snapshot of every slot's (value, s + 1)
     const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
-    return 8 * (ipw * NK + rs * nkw + 64 * nkw + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
+    const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
+    return 8 * (ipw * NK + rs * nkw + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

@@ -292,14 +292,18 @@ void brc_step(const Params* __restrict__ pp) {
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
     uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV, RS, LEAN) / 8);
     uint64_t* s_act = s_meta + IPW * NK;
-    uint64_t* s_dbits = s_act + RS * nkw;        // this step's deliveries, per lane
-    T* s_hm = (T*)(s_dbits + 64 * nkw);          // s_hm[v*64 + lane]: hosts that delivered value v
+    // this step's deliveries, per lane: LDS, or (DBG: lean SPEC, whose LDS limits residency) one
+    // HBM row per wave written once per key word from a register (dacc) -- no LDS at all
+    constexpr bool DBG = LEAN && SPEC;
+    const uint32_t dbw = DBG ? 0u : 64u * nkw;    // LDS u64 words of the delivery bitmap
+    uint64_t* s_dbits = s_act + RS * nkw;
+    T* s_hm = (T*)(s_dbits + dbw);               // s_hm[v*64 + lane]: hosts that delivered value v
     T* s_seen = s_hm;                            // SPEC, NV > 1: s_seen[q*64 + lane]: hosts delivered for phase slot q
     // SPEC: s_cnt[q*64 + lane] = #origins | #"0" << 10 | #"1" << 20 for phase slot q
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));
-    T* s_L = (T*)(s_dbits + 64 * nkw + h_words); // s_L[j*64 + lane]: senders at the j-th delay of dset
+    T* s_L = (T*)(s_dbits + dbw + h_words);      // s_L[j*64 + lane]: senders at the j-th delay of dset
     // gen | GEN16_RESTRICTED (lean kernels keep no generations: no area)
-    uint16_t* s_gen = (uint16_t*)(s_dbits + 64 * nkw + h_words + l_words);
+    uint16_t* s_gen = (uint16_t*)(s_dbits + dbw + h_words + l_words);
     uint16_t* s_klist = s_gen + (LEAN ? 0u : ((IPW * NK + 3) & ~3u));        // this step's active key slots
     // consensus phase: the key list is dead, and its area holds snap[IPW*NK] = value << 14 | (s + 1) of
     // every slot as the BRB phase left it.  A replica's phase change reallocates its own slot
@@ -329,7 +333,7 @@ void brc_step(const Params* __restrict__ pp) {
             if (!LEAN) s_gen[i] = gen16(g32);
         }
         for (uint32_t i = lane; i < RS * nkw; i += 64) s_act[i] = gp(P.act)[item * RS * nkw + i];
-        for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
+        if (!DBG) for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
     }
     uint32_t any_rows = uni32(gp(P.actany)[item]);   // ring rows holding any marked key (wave-uniform)
     uint32_t lane_rows = 0;                      // rows marked by per-lane sends, merged per step
@@ -429,6 +433,8 @@ void brc_step(const Params* __restrict__ pp) {
     };
     // cell (k, lane) at [k * CW * 64] (CONN send rings: ECHO at + 64, + 128, READY at + 192, + 256)
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
+    // lean SPEC: this wave's HBM delivery-bitmap row, word w at [w * 64]
+    const gptr_t<uint64_t> gdbits = gp(P.dbits) + item * (uint64_t)nkw * 64 + lane;
     // lean kernels: compact u32 cells (brc_internal.h C32_*), row k at [k * 64]
     const gptr_t<uint32_t> ccells = gp((uint32_t*)P.cells) + item * (uint64_t)(NK + 1) * 64;
     // lean: this lane's own key slots (bit s mod Q) allocated since the last flush; the wave
@@ -804,6 +810,8 @@ void brc_step(const Params* __restrict__ pp) {
         // The ring row becomes a key list (marks made now land on other rows, so it is fixed);
         // keys come CHUNK at a time and the next chunk's cell words load while one is processed.
         const uint32_t cells0 = st_cells;
+        uint64_t dacc = 0;                           // DBG: deliveries of key word dcur (this lane)
+        uint32_t dcur = NOKEY, dwm = 0;              // DBG: word being filled, words written this step
         uint32_t nkeys = 0;
         for (uint32_t w = 0; w < nkw; ++w) {
             const uint64_t bits = uni64(s_act[row * nkw + w]);
@@ -952,7 +960,17 @@ void brc_step(const Params* __restrict__ pp) {
                 st_bcast += es + rs;
             }
             if (__ballot(dl != 0)) {
-                atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], (uint64_t)dl << (k & 63));
+                if constexpr (DBG) {
+                    // keys come in ascending slot order: a word is complete when the next word starts
+                    const uint32_t wk = k >> 6;
+                    if (wk != dcur) {
+                        if (dcur != NOKEY) { gdbits[dcur * 64] = dacc; dwm |= 1u << dcur; }
+                        dacc = 0; dcur = wk;
+                    }
+                    dacc |= (uint64_t)dl << (k & 63);
+                } else {
+                    atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], (uint64_t)dl << (k & 63));
+                }
                 st_del += dl;
             }
             if (EV) {
@@ -1176,6 +1194,9 @@ void brc_step(const Params* __restrict__ pp) {
                 });
             }
         }
+        if constexpr (DBG) {
+            if (dcur != NOKEY) { gdbits[dcur * 64] = dacc; dwm |= 1u << dcur; }
+        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(1);
 
@@ -1190,8 +1211,13 @@ void brc_step(const Params* __restrict__ pp) {
             const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
 #pragma unroll 1
             for (uint32_t w = 0; w < nkw; ++w) {
-                uint64_t bits = s_dbits[w * 64 + lane];
-                s_dbits[w * 64 + lane] = 0;
+                uint64_t bits;
+                if constexpr (DBG) {
+                    bits = ((dwm >> w) & 1u) ? gdbits[w * 64] : 0ull;   // words written this step only
+                } else {
+                    bits = s_dbits[w * 64 + lane];
+                    s_dbits[w * 64 + lane] = 0;
+                }
                 if (!cons) bits = 0;
                 // one delivery per iteration, ascending slot = ascending (origin, variant); the slots
                 // of one key prefix hold its phase indices mod Q, so when several of them deliver in

@@ -66,6 +66,29 @@ template <int NPAD, typename T> __device__ __forceinline__ T seg_or(T x) {
 
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return x ? 32u - (uint32_t)__clz(x) : 0u; }
 
+// Slot groups of G in {2, 4, 8} consecutive bits of a 64-bit key word: fold_groups leaves bit G*i set
+// iff group i has a set bit; compress_groups packs those bits (multiples of G) to bits 0 .. 64/G - 1.
+__device__ __forceinline__ uint64_t fold_groups(uint64_t x, uint32_t G) {
+    if (G == 2) return (x | (x >> 1)) & 0x5555555555555555ull;
+    if (G == 4) return (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
+    x |= x >> 1; x |= x >> 2; x |= x >> 4;
+    return x & 0x0101010101010101ull;
+}
+__device__ __forceinline__ uint64_t compress_groups(uint64_t x, uint32_t G) {
+    if (G == 2) {
+        x = (x | (x >> 1)) & 0x3333333333333333ull; x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull; x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+        return (x | (x >> 16)) & 0xFFFFFFFFull;
+    }
+    if (G == 4) {
+        x = (x | (x >> 3)) & 0x0303030303030303ull; x = (x | (x >> 6)) & 0x000F000F000F000Full;
+        x = (x | (x >> 12)) & 0x000000FF000000FFull;
+        return (x | (x >> 24)) & 0xFFFFull;
+    }
+    x = (x | (x >> 7)) & 0x0003000300030003ull; x = (x | (x >> 14)) & 0x0000000F0000000Full;
+    return (x | (x >> 28)) & 0xFFull;
+}
+
 // compile-time unrolled loop: f(IC<0>{}), ..., f(IC<N-1>{}) (register arrays stay statically indexed)
 template <int I> struct IC { static constexpr int value = I; };
 template <int N> struct Unrolled {
@@ -1219,6 +1242,43 @@ void brc_step(const Params* __restrict__ pp) {
                     s_dbits[w * 64 + lane] = 0;
                 }
                 if (!cons) bits = 0;
+                if constexpr (LEAN && !SPEC) {
+                    // A lane whose deliveries in this word can change no phase (fewer than T_cnt - vcount
+                    // of them, or not in phase 1 / 2) and hit each key prefix at most once takes them all
+                    // at once: the value sets gain the hosts (an origin is Q * NV consecutive slots),
+                    // vcount the count, and values new to `order` enter by first slot (= delivery order).
+                    // The others (a phase change, or two phases of one key in one step) go one by one.
+                    if (__ballot(bits != 0)) {
+                        const uint32_t sv = (uint32_t)s_snap[w * 64 + lane] >> 14;   // slot w*64+lane's value
+                        const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
+                        const uint32_t nb = (uint32_t)__popcll(bits);
+                        const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
+                        if (nb && oneper && ((phase != 1 && phase != 2) || vcount + nb < P.T_cnt)) {
+                            const uint32_t G = Q * NV, opw = 64u / G;
+                            uint32_t first[4];
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) {
+                                const uint64_t dv = bits & vm[v];
+                                first[v] = dv ? (uint32_t)__ffsll((unsigned long long)dv) - 1u : 64u;
+                                if (dv) s_hm[v * 64 + lane] |= (T)(compress_groups(fold_groups(dv, G), G) << (w * opw));
+                                // already inserted? (the field test of cons_deliver_vh)
+                                const uint32_t xo = order ^ ((uint32_t)v * 0x55u);
+                                if (((~(xo | (xo >> 1)) & 0x55u & ((1u << (2 * nvals)) - 1u)) != 0)) first[v] = 64u;
+                            }
+                            for (int r = 0; r < 4; ++r) {       // new values, by first delivery
+                                uint32_t bv = 0, bp = 64u;
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) if (first[v] < bp) { bp = first[v]; bv = (uint32_t)v; }
+                                if (bp == 64u) break;
+                                order |= bv << (2 * nvals); ++nvals;
+#pragma unroll
+                                for (int v = 0; v < 4; ++v) if ((uint32_t)v == bv) first[v] = 64u;   // static indices
+                            }
+                            vcount += nb;
+                            bits = 0;
+                        }
+                    }
+                }
                 // one delivery per iteration, ascending slot = ascending (origin, variant); the slots
                 // of one key prefix hold its phase indices mod Q, so when several of them deliver in
                 // the same step (rare) the smallest phase index goes first

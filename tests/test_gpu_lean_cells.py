@@ -102,3 +102,29 @@ def test_repeated_resets_wrap_slot_tags():
                         assert r[k] == exp[k], "%s %s" % (sp["name"], k)
             else:
                 assert snap == first, "pass %d differs from the first" % p
+
+
+# Q = 4 holds one round of phase indices (a second round reuses slots still in flight: BRC_OVERFLOW,
+# which the oracle does not model), Q = 8 two rounds
+@pytest.mark.parametrize("nv,window,rcap", [(1, 4, 1), (1, 8, 2), (2, 4, 1)])
+def test_reference_consensus_windows_and_variants_vs_oracle(runner, nv, window, rcap):
+    """Reference-protocol consensus on the lean kernel with each key window and, with two key
+    variants, equivocating Byzantine senders: the consensus pass takes a word's deliveries at
+    once when they can change no phase (fold_groups / compress_groups over Q * NV slots per
+    origin) and one by one otherwise; both must equal the oracle's message-by-message run."""
+    n, f = 40, 13
+    byz = list(range(35, 40)) if nv == 2 else []
+    specs = []
+    for g in range(12):
+        sp = S.cons_spec(n, f, 0xB01C + window, 0 if g % 2 else 2, 1 if g % 2 else 8, 4100 + g, round_cap=rcap,
+                         byzantine=byz, nv=nv, extra=S.equivocation_actions(n, byz) if byz else ())
+        sp["name"] = "lean-cons-q%d-nv%d/%d" % (window, nv, g)
+        specs.append(sp)
+    groups = {}
+    for sp in specs:                                     # one batch per delay model (consecutive ids)
+        groups.setdefault(sp["delay_model"], []).append(sp)
+    for batch in groups.values():
+        got = []
+        for sp in batch:                                 # ids are not consecutive inside a model group
+            got += runner.run_batch([sp], key_window=window)
+        _check(got, batch)

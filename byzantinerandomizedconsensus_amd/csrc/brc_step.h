@@ -1242,6 +1242,40 @@ void brc_step(const Params* __restrict__ pp) {
                     s_dbits[w * 64 + lane] = 0;
                 }
                 if (!cons) bits = 0;
+                if constexpr (LEAN && SPEC) {
+                    // SPEC (one key variant per origin): when every lane with deliveries in this word is
+                    // at the same phase index c0, the slots' phase indices classify against c0 with
+                    // ballots (lane = slot). A lane whose current-phase deliveries cannot complete the
+                    // phase (spec_advance acts only at n - f origins) adds the word's deliveries to its
+                    // phase-slot counts at once; the others go one by one.
+                    const uint64_t hb = __ballot(bits != 0);
+                    if (!seen_on && hb) {
+                        const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
+                        const uint32_t c0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)hb) - 1));
+                        if (!__ballot(bits != 0 && cur != c0)) {
+                            const uint32_t sn = s_snap[w * 64 + lane];
+                            const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;   // slot w*64+lane
+                            const uint64_t inw = __ballot(ss >= c0 && ss - c0 < Q), atc = __ballot(ss == c0);
+                            const uint64_t past = __ballot(ss != 0xFFFFFFFFu && ss >= c0 && ss - c0 >= Q);
+                            const uint64_t v1 = __ballot(sv == 1), v2 = __ballot(sv == 2);
+                            const uint32_t ncur = (uint32_t)__popcll(bits & atc);
+                            const uint32_t qc = c0 & Qm;
+                            if (bits && (round == 0 || (s_cnt[qc * 64 + lane] & 0x3FFu) + ncur < n - P.f)) {
+                                if (bits & past) ovf = true;                  // beyond the window (spec_deliver)
+                                const uint64_t b = bits & inw;
+                                // slots of phase slot q (slot mod Q == q): bit q of every Q-bit group
+                                const uint64_t g0 = Q == 2 ? 0x5555555555555555ull : Q == 4 ? 0x1111111111111111ull
+                                                                                    : 0x0101010101010101ull;
+                                for (uint32_t q = 0; q < Q; ++q) {
+                                    const uint64_t bq = b & (g0 << q);
+                                    if (bq) s_cnt[q * 64 + lane] += (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
+                                                                     ((uint32_t)__popcll(bq & v2) << 20);
+                                }
+                                bits = 0;
+                            }
+                        }
+                    }
+                }
                 if constexpr (LEAN && !SPEC) {
                     // A lane whose deliveries in this word can change no phase (fewer than T_cnt - vcount
                     // of them, or not in phase 1 / 2) and hit each key prefix at most once takes them all

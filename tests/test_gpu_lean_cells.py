@@ -128,3 +128,18 @@ def test_reference_consensus_windows_and_variants_vs_oracle(runner, nv, window, 
         for sp in batch:                                 # ids are not consecutive inside a model group
             got += runner.run_batch([sp], key_window=window)
         _check(got, batch)
+
+
+@pytest.mark.parametrize("window,model,dmax", [(4, 1, 3), (8, 2, 8), (8, 3, 6)])
+def test_spec_consensus_word_at_once_vs_oracle(runner, window, model, dmax):
+    """SPEC consensus on the lean kernel (n = 48): the consensus pass adds a word's deliveries to
+    the phase-slot counts at once when every delivering lane is at one phase index and none can
+    complete its phase, one by one otherwise; coin rounds keep phases apart across replicas."""
+    specs = []
+    for g in range(8):
+        sp = S.spec_cons_spec(48, 15, 0x5EC48 + window, model, dmax, 900 + g, round_cap=3, window=window,
+                              coin_seed=0xC0DE)
+        sp["name"] = "lean-spec-bulk-q%d/%d" % (window, g)
+        specs.append(sp)
+    got = runner.run_specs(specs)
+    _check(got, specs)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dev-only: per-section cycle split of the lean step kernel on the cfg4 workload.
 Needs a variant built with -DBRC_STAMPS (tools/variant.py stamps -DBRC_STAMPS); run with
-BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances]."""
+BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances] [reference|spec]."""
 import ctypes
 import os
 import sys
@@ -11,8 +11,10 @@ from byzantinerandomizedconsensus_amd import _lib as L  # noqa: E402
 from byzantinerandomizedconsensus_amd.engine import Engine  # noqa: E402
 
 inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
+spec = len(sys.argv) > 2 and sys.argv[2] == "spec"
 eng = Engine(n=64, f=21, instances=inst, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET,
-             delay_max=8, round_cap=1, step_cap=4000, key_window=4, variants=1, proposals=L.PROPOSALS_PHILOX)
+             delay_max=8, round_cap=1, step_cap=4000, key_window=8 if spec else 4, variants=1,
+             proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
 out = (ctypes.c_ulonglong * 8)()
 eng.reset(); eng.run()

@@ -284,6 +284,19 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:     # N = 1 only
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, head_mode, 8 if head_mode == "spec" else 4,
                                            args.round_cap)
+    if rank == 0 and head_mode == "reference" and args.round_cap == 1:
+        # the reference's own Python path cannot travel to the GPU box: its rate on this workload was
+        # measured in the build container (tools/ref_cpu_rate.py) and is reported beside, not as, the baseline
+        try:
+            with open(os.path.join(ROOT, "profiles", "ref_cpu_rate.json")) as fh:
+                r = json.load(fh)
+            out["reference_python_rate"] = {
+                "value": r["per_core_instances_per_s"], "unit": "decided instances/s per core",
+                "cores": 1, "sample": "%d cfg4 instances, one process per core, %s CPUs, Python %s" % (
+                    r["instances"], r["cpus_visible"], r["python"]),
+                "source": "profiles/ref_cpu_rate.json (build container, not this host)"}
+        except (OSError, ValueError, KeyError):
+            pass
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:

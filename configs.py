@@ -12,7 +12,9 @@ Workloads:
   cfg3       1,000,000 instances n=16 f=5, Byzantine {11..15} equivocating, uniform delays [1,4]
   cfg2-spec, cfg3-spec   the same two in SPEC mode (the reference protocol stalls on most of them)
   cfg4-ref   2^20 instances per GPU n=64 f=21, slow-set delays D=8 (the bench.py workload)
-  cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^19 instances per GPU
+  cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^20 instances per GPU
+  cfg4-conn  the same with connection-identity peers (what the shipped reference runs), 2^18
+  cfg4-beb   the reference consensus over best-effort broadcast (BRC_MODE_BEB), 2^20
   cfg5-*     n=256 f=85 SPEC, 2048 instances per GPU, const / uniform[1,4] / geometric<=16
 
 A step is one pass of the hot path over the batch (reset + run to completion); the timed region
@@ -54,6 +56,12 @@ def workloads(L):
         "cfg4-spec": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                           round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
     }
+    # cfg4 under the peer identity the shipped reference runs (core/brbroadcast.py:69: every message
+    # is a new connection, no duplicate suppression; 5-word cells) and over best-effort broadcast
+    W["cfg4-conn"] = (1 << 18, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                          round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
+    W["cfg4-beb"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                         round_cap=1, key_window=8, mode=L.MODE_BEB))
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
         W["cfg5-" + name] = (2048, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
                                              delay_max=dmax, round_cap=1, key_window=8, mode=L.MODE_SPEC,
@@ -63,8 +71,10 @@ def workloads(L):
 
 def cell_bytes(n, peer_mode=0):
     """Bytes of one (receiver, key) cell: 4 on the lean kernels (33 <= n <= 64, sender peers:
-    brc_internal.h C32_*), 8 on the others."""
-    return 4 if 32 < n <= 64 and peer_mode == 0 else 8
+    brc_internal.h C32_*), 40 with connection peers, 8 on the others."""
+    if peer_mode:
+        return 40                    # connection peers: the cell + two 16-step send-count rings
+    return 4 if 32 < n <= 64 else 8
 
 
 def measured_traffic(name, kernel_ms):

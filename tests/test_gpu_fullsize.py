@@ -173,15 +173,18 @@ def test_cfg5_n256_full_size(model, dmax):
             assert (rep["first_decide_round"], rep["first_decide_t"]) == (exp[0], exp[1]), (model, g, d)
 
 
-def test_cfg4_bench_batch_2p20_sampled():
-    """The bench's own batch (2^20 instances, reference protocol): instances sampled across the
-    whole id range equal the oracle run alone on their global id."""
+@pytest.mark.parametrize("mode", ["reference", "spec"])
+def test_cfg4_bench_batch_2p20_sampled(mode):
+    """The bench's own batches (2^20 instances in one launch: the reference protocol, and SPEC with
+    Q = 8 on 4-byte cells): instances sampled across the whole id range equal the oracle run alone
+    on their global id."""
     L = _L()
     N = 1 << 20
+    spec = mode == "spec"
     kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
-              round_cap=1, step_cap=4000, key_window=4, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_REFERENCE,
-              coin_seed=0xC017C017)
-    ids = sorted(random.Random(20).sample(range(N), 24)) + [N - 1]
+              round_cap=1, step_cap=4000, key_window=8 if spec else 4, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    ids = sorted(random.Random(20).sample(range(N), 12 if spec else 24)) + [N - 1]
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
         hist = eng.round_histogram(66)
@@ -189,7 +192,10 @@ def test_cfg4_bench_batch_2p20_sampled():
         reps = {i: eng.replicas(i, 1)[0] for i in ids}
     assert hist[0] == 0 and sum(hist) == N, "every instance decided"
     for g in ids:
-        exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1))
+        if spec:
+            exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1, window=8, coin_seed=0xC017C017))
+        else:
+            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1))
         for k in KEYS:
             assert res[g][k] == exp[k], (g, k)
         first = {}

@@ -245,7 +245,7 @@ static int clear_state(Engine* e, bool full) {
                            (uint64_t)keys);
         HIPCHK(e, hipGetLastError());
     }
-    HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->actany, 0, (size_t)e->nitems * 4, e->stream));
     HIPCHK(e, hipMemsetAsync(e->items, 0, (size_t)e->nitems * sizeof(ItemState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->inst, 0, (size_t)e->cfg.instances * sizeof(InstState), e->stream));
@@ -396,7 +396,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
-        {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * 8},
+        {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},

@@ -107,8 +107,13 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
     return spec ? (Q * 64 * (nv > 1 ? msize : 0u) + Q * 64 * 4 + 7) / 8 : (4 * 64 * msize + 7) / 8;
 }
 
+// Activity-ring words per (row, key word): the lean kernels keep one ECHO and one READY row (typed
+// marks: a key step evaluates only the message types that can land; SEND arrivals are found from the
+// key metadata), the others one untyped row.
+__host__ __device__ constexpr uint32_t act_types(bool lean) { return lean ? 2u : 1u; }
+
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
-// meta[IPW*NK] u64 | act[RS][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
+// meta[IPW*NK] u64 | act[RS][act_types][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u16 (not on the lean kernels) | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
 // reused as the consensus snapshot snap[IPW*NK] u16)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
@@ -121,7 +126,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
-    return 8 * (ipw * NK + rs * nkw + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
+    return 8 * (ipw * NK + rs * nkw * act_types(lean) + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

@@ -37,6 +37,8 @@
 namespace brc {
 
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
+// lean key-list entries: key slot (< 2^12) | the message types that can land on it this step << TB_SH
+constexpr uint32_t TB_S = 1, TB_E = 2, TB_R = 4, TB_SH = 12, TB_KEY = (1u << TB_SH) - 1u;
 
 template <int NPAD> struct MaskOf { using type = uint64_t; };
 template <> struct MaskOf<4> { using type = uint8_t; };
@@ -296,6 +298,7 @@ void brc_step(const Params* __restrict__ pp) {
     using T = typename MaskOf<NPAD>::type;
     constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
     constexpr int IPW = 64 / NPAD;
+    constexpr uint32_t AT = act_types(LEAN);     // activity-ring words per (row, key word)
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
     // wid via readfirstlane: the item (and every address derived from it) is then provably wave-uniform
@@ -319,7 +322,7 @@ void brc_step(const Params* __restrict__ pp) {
     // HBM row per wave written once per key word from a register (dacc) -- no LDS at all
     constexpr bool DBG = LEAN && SPEC;
     const uint32_t dbw = DBG ? 0u : 64u * nkw;    // LDS u64 words of the delivery bitmap
-    uint64_t* s_dbits = s_act + RS * nkw;
+    uint64_t* s_dbits = s_act + RS * nkw * AT;
     T* s_hm = (T*)(s_dbits + dbw);               // s_hm[v*64 + lane]: hosts that delivered value v
     T* s_seen = s_hm;                            // SPEC, NV > 1: s_seen[q*64 + lane]: hosts delivered for phase slot q
     // SPEC: s_cnt[q*64 + lane] = #origins | #"0" << 10 | #"1" << 20 for phase slot q
@@ -355,7 +358,7 @@ void brc_step(const Params* __restrict__ pp) {
             s_meta[i] = ok ? gp(P.meta)[mb + i] | ((LEAN && (g32 & GEN_RESTRICTED)) ? M_RESTRICTED : 0ull) : 0ull;
             if (!LEAN) s_gen[i] = gen16(g32);
         }
-        for (uint32_t i = lane; i < RS * nkw; i += 64) s_act[i] = gp(P.act)[item * RS * nkw + i];
+        for (uint32_t i = lane; i < RS * nkw * AT; i += 64) s_act[i] = gp(P.act)[item * RS * nkw * AT + i];
         if (!DBG) for (uint32_t w = 0; w < nkw; ++w) s_dbits[w * 64 + lane] = 0;
     }
     uint32_t any_rows = uni32(gp(P.actany)[item]);   // ring rows holding any marked key (wave-uniform)
@@ -369,6 +372,11 @@ void brc_step(const Params* __restrict__ pp) {
     const uint64_t byzm = iex ? gp(P.byz)[inst] : ~0ull;
     const bool real = iex && (uint32_t)d < n;
     const bool honest = real && !((byzm >> d) & 1ull);
+    // lane masks: a wave-uniform 64-bit mask turns back into a per-lane predicate at no cost
+    // (inverse ballot: the SGPR pair is the lane mask), where a bool kept across blocks is
+    // re-materialised with a select and a compare at every ballot
+    const uint64_t hon_mask = uni64(__ballot(honest));
+    auto lane_in = [](uint64_t mask) -> bool { return __builtin_amdgcn_inverse_ballot_w64(mask); };
 
     // ---- link-delay masks: L[i] = senders j whose link j -> d has delay i+1 (schedule.h)
     T L[DM];
@@ -449,6 +457,8 @@ void brc_step(const Params* __restrict__ pp) {
             if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
+    // lean ring marks (process_pair): lane L < 8 marks for delay class L & 1
+    const uint64_t mk_ov = (lane & 1) ? OV1 : OV0;
     // the j-th delay mask present in the wave (j < ndl)
     auto Lmask = [&](uint32_t j) -> T {
         if constexpr (NLR != 0) return j == 0 ? RL0 : RL1;
@@ -530,14 +540,30 @@ void brc_step(const Params* __restrict__ pp) {
             }
         }
     };
-    // key k may have arrivals at t + i + 1 for every bit i of ds (called by individual lanes)
-    auto mark_lane = [&](uint32_t k, uint32_t ds) {
+    // key k may have arrivals of message type ty (BRC_SEND / BRC_ECHO / BRC_READY) at t + i + 1 for
+    // every bit i of ds (called by individual lanes).  Lean kernels: typed rows (ECHO row, READY row);
+    // a SEND leaves no key mark there (the key list finds SEND arrivals from the key metadata), only
+    // the row bit that makes the step loop visit that step.
+    auto mark_lane = [&](uint32_t k, uint32_t ds, uint32_t ty) {
         while (ds) {
             const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
             const uint32_t row = (t + i + 1) & (RS - 1);
-            atomicOr((unsigned long long*)&s_act[row * nkw + (k >> 6)], 1ull << (k & 63));
+            if (!LEAN || ty != BRC_SEND)
+                atomicOr((unsigned long long*)&s_act[(row * AT + (LEAN ? ty - BRC_ECHO : 0u)) * nkw + (k >> 6)],
+                         1ull << (k & 63));
             lane_rows |= 1u << row;
         }
+    };
+    // lean kernels: does key slot k still have ECHO / READY arrivals pending?  Every ring row but the
+    // current one holds only future marks (a marked row is always visited and cleared), so the key
+    // loop keeps no per-key t_quiet for them; t_quiet in the metadata covers the SEND alone.
+    auto ring_busy = [&](uint32_t k) -> bool {
+        const uint32_t kw = k >> 6, cur = t & (RS - 1);
+        uint64_t acc = 0;
+#pragma unroll 1
+        for (uint32_t r = 0; r < RS; ++r)
+            if (r != cur) acc |= s_act[(r * AT + 0) * nkw + kw] | s_act[(r * AT + 1) * nkw + kw];
+        return (acc >> (k & 63)) & 1ull;
     };
     // honest origin d broadcasts SEND for its key (d, s) with value v
     // (core/byzantinerandomizedconsensus.py:48-50 / :80-83 / :102-106, base/broadcast.py:30-35)
@@ -545,11 +571,11 @@ void brc_step(const Params* __restrict__ pp) {
         const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint64_t m = s_meta[mbase + k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
-        if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
+        if ((m_s1(m) != 0 && (t < m_tquiet(m) || (LEAN && ring_busy(k)))) || s >= P.s_limit) { ovf = true; return; }
         if (!LEAN) s_gen[mbase + k] = (uint16_t)(((s_gen[mbase + k] & GEN_MASK) + 1) & GEN_MASK);
         if (LEAN) clr |= 1u << (s & Qm);                 // compact cells: the row is rewritten fresh
         s_meta[mbase + k] = m_pack(s + 1, t, t + maxout, d, v);
-        mark_lane(k, outset);
+        mark_lane(k, outset, BRC_SEND);
         q_until = max(q_until, t + maxout);
         st_msgs += n;
         st_smax = max(st_smax, s);
@@ -694,7 +720,7 @@ void brc_step(const Params* __restrict__ pp) {
                         uint64_t m = s_meta[mbase + k];
                         uint32_t gen = LEAN ? 0u : s_gen[mbase + k] & GEN_MASK;
                         const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
-                        if ((!declared && m_s1(m) != 0 && t < m_tquiet(m)) || r.s >= P.s_limit) {
+                        if ((!declared && m_s1(m) != 0 && (t < m_tquiet(m) || (LEAN && ring_busy(k)))) || r.s >= P.s_limit) {
                             ovf = true;
                         } else {
                             uint32_t tq = m_tquiet(m);
@@ -709,7 +735,7 @@ void brc_step(const Params* __restrict__ pp) {
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 gp(P.kdst)[inst * NK + k] = r.dst;
-                                mark_lane(k, os);
+                                mark_lane(k, os, BRC_SEND);
                                 st_msgs += __popcll(r.dst & all64);
                                 log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
                             }
@@ -776,7 +802,7 @@ void brc_step(const Params* __restrict__ pp) {
                 }
                 const uint32_t os = wave_or(sent ? outset : 0u);
                 if (os) {
-                    if (lane == 0) mark_lane(k, os);
+                    if (lane == 0) mark_lane(k, os, r.type);
                     const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
                     if (mine && myq) {
                         if (d == 0) {
@@ -833,14 +859,35 @@ void brc_step(const Params* __restrict__ pp) {
         // The ring row becomes a key list (marks made now land on other rows, so it is fixed);
         // keys come CHUNK at a time and the next chunk's cell words load while one is processed.
         const uint32_t cells0 = st_cells;
-        uint64_t dacc = 0;                           // DBG: deliveries of key word dcur (this lane)
-        uint32_t dcur = NOKEY, dwm = 0;              // DBG: word being filled, words written this step
+        // lean: this step's deliveries are collected per key word in a register (dacc, word dcur) and
+        // stored once when the next word starts: LDS, or (DBG) the wave's HBM row; dwm = words written
+        uint64_t dacc = 0;
+        uint32_t dcur = NOKEY, dwm = 0;
+        auto flush_dacc = [&](uint32_t wk, uint64_t v) {
+            if constexpr (DBG) gdbits[wk * 64] = v;
+            else s_dbits[wk * 64 + lane] = v;
+            dwm |= 1u << wk;
+        };
         uint32_t nkeys = 0;
         for (uint32_t w = 0; w < nkw; ++w) {
-            const uint64_t bits = uni64(s_act[row * nkw + w]);
+            uint64_t bits;
+            uint32_t tb = 0;                         // lean: message types that can land on slot w*64+lane
+            if constexpr (LEAN) {
+                // typed marks: ECHO / READY rows; SEND arrivals from the slot's metadata -- the SEND of
+                // slot k lands now at some receiver iff t - t_send is a delay of its sender's outset
+                const uint64_t mE = uni64(s_act[(row * AT + 0) * nkw + w]), mR = uni64(s_act[(row * AT + 1) * nkw + w]);
+                const uint64_t m = s_meta[w * 64 + lane];
+                const uint32_t dt1 = t - m_tsend(m) - 1u;                  // delay - 1 of a SEND landing now
+                const uint32_t os = (uint32_t)__shfl((int)outset, (int)m_sender(m));
+                const bool sl = m_s1(m) != 0 && dt1 < 32u && ((os >> (dt1 & 31u)) & 1u);
+                tb = (sl ? TB_S : 0u) | ((uint32_t)(mE >> lane) & 1u) * TB_E | ((uint32_t)(mR >> lane) & 1u) * TB_R;
+                bits = __ballot(tb != 0);
+            } else {
+                bits = uni64(s_act[row * nkw + w]);
+            }
             const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
-            if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)(w * 64 + lane);
+            if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)((w * 64 + lane) | (tb << TB_SH));
             nkeys += (uint32_t)__popcll(bits);
         }
         if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
@@ -864,166 +911,229 @@ void brc_step(const Params* __restrict__ pp) {
         // wraps to a huge value (matching no 7-bit offset) for a delay reaching before the epoch
         const uint32_t ts = t - ep;
         const uint32_t tm0 = ts - dly0, tm1 = ndl > 1 ? ts - dly1 : 0x10000u;   // 0x10000: no 7-bit offset
-        auto process_lean = [&](const uint32_t k, const uint64_t m, const uint32_t lo, uint32_t& nw, bool& wr) {
-            if (m_s1(m) == 0) { ++nk_skip; return; }            // the slot holds no key
-            BRC_KCOUNT(0);
-            // lanes that are not real replicas and Byzantine lanes never update their cells here, so
-            // their words keep the fresh row's "never sent" unless an injection sent for them
-            const uint32_t tE = (lo >> C32_OE_SH) & 127u, tR = lo >> C32_OR_SH;   // offsets: SENT ECHO / READY
-            // arrivals: senders whose message lands now, per delay present (empty ballots skipped)
-            uint32_t ea = 0, ra = 0;
-            uint64_t be_any = 0, br_any = 0;
+        // A key-list entry carries the message types that can land on its key this step (TB_*): only
+        // those are evaluated.  Keys go in PAIRS: the scalar work (type dispatch, early exits, ring
+        // marks) is shared by two keys, while each key's per-lane work is its own -- the CU's scalar
+        // unit, not the SIMDs, bounds this loop.  The loop carries little state from key to key:
+        // ring rows and q_until are derived from the ring once per step (below), the cell statistics
+        // st_cells, st_del and st_bcast are wave-uniform popcounts of ballots, st_arr is per lane.
+        // NLR: the ring word lane L < 8 marks for a pair (key word added per key): the row at t + delay
+        // of class L & 1, type (L >> 1) & 1; mk_ov = the senders with a link of that class
+        const uint32_t mk_row = ((t + ((lane & 1) ? dly1 : dly0)) & (RS - 1)) * AT * nkw + ((lane >> 1) & 1) * nkw;
+        // senders whose message of one type, sent at offset tx, lands on this receiver now
+        auto count = [&](uint32_t tx) -> uint32_t {
             if constexpr (NLR != 0) {
-                // for an honest receiver the delay classes partition the real senders (every link
-                // has one of the delays present: RL1 = real & ~RL0, and with one delay tm1 matches
-                // nothing), so each count is ONE popcount of a bitfield merge (v_bfi)
-                const uint64_t be0 = __ballot(tE == tm0), br0 = __ballot(tR == tm0);
-                const uint64_t be1 = __ballot(tE == tm1), br1 = __ballot(tR == tm1);
-                // (b0 & RL0) | (b1 & ~RL0) == b1 ^ ((b0 ^ b1) & RL0): the XOR of the two ballots is
-                // scalar, leaving two VALU ops per 32-bit half (-0.45 % kernel, A/B)
-                ea = popc(be1 ^ ((be0 ^ be1) & RL0));
-                ra = popc(br1 ^ ((br0 ^ br1) & RL0));
-                be_any = be0 | be1; br_any = br0 | br1;
+                // for an honest receiver the delay classes partition the real senders (RL1 = real &
+                // ~RL0; with one delay tm1 matches nothing): ONE popcount of a bitfield merge
+                const uint64_t b0 = __ballot(tx == tm0), b1 = __ballot(tx == tm1);
+                return popc(b1 ^ ((b0 ^ b1) & RL0));
             } else {
-                const uint32_t dE = ts - tE, dR = ts - tR;      // C32_OLD / C32_NEVER: no delay
+                const uint32_t dx = ts - tx;                     // C32_OLD / C32_NEVER: no delay
+                uint32_t c = 0;
                 Unrolled<DM>::run([&](auto jc) {
                     constexpr int j = decltype(jc)::value;
                     if ((uint32_t)j < ndl) {
-                        const uint32_t dly = (dlist >> (4 * j)) & 15u;
-                        const uint64_t be = __ballot(dE == dly + 1u), br = __ballot(dR == dly + 1u);
-                        if (be | br) {
-                            const T Lj = s_L[j * 64 + lane];
-                            ea += popc(be & Lj);
-                            ra += popc(br & Lj);
-                        }
-                        be_any |= be; br_any |= br;
+                        const uint64_t b = __ballot(dx == ((dlist >> (4 * j)) & 15u) + 1u);
+                        if (b) c += popc(b & s_L[j * 64 + lane]);
                     }
                 });
+                return c;
             }
-            // SEND from the key's origin: arrives at t_send + delay(origin -> d)
-            bool s_arr = false;
-            const uint32_t dt = t - m_tsend(m);
-            bool s_win;
-            uint32_t sj = 0;                                     // index of delay dt among those present
-            if constexpr (NLR != 0) {
-                s_win = dt == dly0 || (ndl > 1 && dt == dly1);
-                sj = dt == dly0 ? 0u : 1u;
-            } else {
-                s_win = dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);
-                sj = popc(dset & ((1u << ((dt - 1u) & 31)) - 1u));
+        };
+        auto process_pair = [&](const uint32_t (&ent)[2], const uint64_t (&m)[2], const uint32_t (&lo)[2],
+                                uint32_t (&nw)[2], bool (&wr)[2]) {
+            uint32_t k[2], tb[2], tE[2], tR[2], ea[2] = {0u, 0u}, ra[2] = {0u, 0u}, sa[2] = {0u, 0u};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                k[i] = ent[i] & TB_KEY; tb[i] = ent[i] >> TB_SH;
+                // lanes that are not real replicas and Byzantine lanes never update their cells here, so
+                // their words keep the fresh row's "never sent" unless an injection sent for them
+                tE[i] = (lo[i] >> C32_OE_SH) & 127u; tR[i] = lo[i] >> C32_OR_SH;   // offsets: SENT ECHO / READY
             }
-            if (s_win) {
-                bool hit = (Lmask(sj) >> m_sender(m)) & 1;
-                if (m & M_RESTRICTED) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
-                s_arr = honest && hit;
-            }
-            const bool has = honest && (s_arr || ea || ra);
-            if (!__ballot(has)) { BRC_KCOUNT(1); return; }      // nothing lands on this key now
-            // Per-lane work below is branch-free integer arithmetic on 0/1 flags: lane-mask logic
-            // and divergent branches would cost scalar (SALU) instructions, the busier issue port.
-            st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
-            st_cells += has ? 1u : 0u;
-            // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
-            const bool opn = has && !(lo & F_DEL);
-            if (!__ballot(opn)) { BRC_KCOUNT(2); return; }
-            BRC_KCOUNT(3);
-            uint32_t fl = lo & 31u, ec = (lo >> C32_EC_SH) & 63u, rc = (lo >> C32_RC_SH) & 63u;
-            uint32_t es = 0, rs = 0, dl = 0;                     // 0/1: ECHO sent, READY sent, delivered
-            const uint32_t sa = (opn && s_arr) ? 1u : 0u;
-            const uint32_t e = opn ? ea : 0u, r = opn ? ra : 0u;
-            // 1 when a >= b (both < 2^31)
-            auto ge = [](uint32_t a, uint32_t b) -> uint32_t { return ((a - b) >> 31) ^ 1u; };
-            if constexpr (BEB) {
-                bool bes, brs, bdl;
-                brb_cell_update_beb(fl, sa != 0, bes, brs, bdl);
-                dl = bdl ? 1u : 0u;
-            } else if constexpr (SPEC) {
-                bool bes, brs, bdl;
-                brb_cell_update_spec(fl, ec, rc, sa != 0, e, r, T_echo, T_amp, T_del, bes, brs, bdl);
-                es = bes ? 1u : 0u; rs = brs ? 1u : 0u; dl = bdl ? 1u : 0u;
-            } else {
-                // brb_cell_update in integer form; its SEND / ECHO / READY stages run only when some
-                // message of that type lands (the skipped stages are identities).  F_EEX = bit 0,
-                // F_REX = 1, F_DEL = 2, F_ES = 3, F_RS = 4.
-                if (s_win) {                                                     // :76-82
-                    es = sa & ~fl & 1u;                                          // SEND, no ECHO entry
-                    fl |= es | (es << 3);                                        // F_EEX | F_ES
-                }
-                if (be_any) {                                                    // :84-98
-                    const uint32_t eon = min(e, 1u);
-                    const uint32_t chk = min(e + (fl & 1u) - eon, 1u);           // a checked ECHO (:87-89)
-                    fl |= eon;                                                   // F_EEX
-                    ec += e;
-                    const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;   // !F_REX (:95)
-                    fl |= (r1 << 1) | (r1 << 4);                                 // F_REX | F_RS
-                    rs = r1;
-                }
-                if (br_any) {                                                    // :100-119
-                    const uint32_t ron = min(r, 1u);
-                    const uint32_t rex = (fl >> 1) & 1u;
-                    const uint32_t rexm = 0u - rex;                              // all ones iff F_REX
-                    const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = r + (rc & rexm);   // checked sizes
-                    fl |= ron << 1;                                              // F_REX
-                    rc += r;
-                    const uint32_t any = ron & ge(rhi, rlo);
-                    const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
-                    const uint32_t r2 = any & ~fl & ~(fl >> 4) & ge(ahi, alo) & 1u;     // !F_EEX, !F_RS
-                    fl |= r2 << 4;                                               // F_RS
-                    dl = any & ge(rhi, T_del);
-                    fl |= dl << 2;                                               // F_DEL
-                    rs |= r2;
-                }
-            }
-            {   // new word for open cells; the others keep theirs.  A count reaches 64 only when
-                // every sender's message of that type has arrived, so none is compared again: the
-                // stored counts saturate at 63 without changing any later transition
-                nw = fl | (min(ec, 63u) << C32_EC_SH) | (min(rc, 63u) << C32_RC_SH) |
-                     ((es ? ts : tE) << C32_OE_SH) | ((rs ? ts : tR) << C32_OR_SH);
-                wr = opn;
-                st_bcast += es + rs;
-            }
-            if (__ballot(dl != 0)) {
-                if constexpr (DBG) {
-                    // keys come in ascending slot order: a word is complete when the next word starts
-                    const uint32_t wk = k >> 6;
-                    if (wk != dcur) {
-                        if (dcur != NOKEY) { gdbits[dcur * 64] = dacc; dwm |= 1u << dcur; }
-                        dacc = 0; dcur = wk;
+            BRC_KCOUNT(0);
+            // a type that cannot land on one key of the pair counts zero there: exact either way
+            const uint32_t tbu = tb[0] | tb[1];
+            if (tbu & TB_E) { ea[0] = count(tE[0]); ea[1] = count(tE[1]); }
+            if (tbu & TB_R) { ra[0] = count(tR[0]); ra[1] = count(tR[1]); }
+            if (tbu & TB_S) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (tb[i] & TB_S) {
+                        // SEND from the key's origin: lands on d iff delay(origin -> d) == t - t_send, and
+                        // the key list holds the key now only for such a delay of the origin's outset
+                        const uint32_t dt = t - m_tsend(m[i]), snd = m_sender(m[i]);
+                        bool hit;
+                        if constexpr (NLR != 0) {
+                            hit = (((RL0 >> snd) & 1) != 0) == (dt == dly0);
+                        } else {
+                            const uint32_t sj = popc(dset & ((1u << ((dt - 1u) & 31)) - 1u));
+                            hit = (s_L[sj * 64 + lane] >> snd) & 1;
+                        }
+                        uint64_t hm = __ballot(hit) & hon_mask;
+                        if (m[i] & M_RESTRICTED) hm &= __ballot((gp(P.kdst)[inst * NK + k[i]] >> d) & 1ull);
+                        sa[i] = lane_in(hm) ? 1u : 0u;
                     }
-                    dacc |= (uint64_t)dl << (k & 63);
-                } else {
-                    atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], (uint64_t)dl << (k & 63));
                 }
-                st_del += dl;
+            }
+            uint64_t ob[2];
+            uint32_t arr2 = 0;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint32_t arr = ea[i] + ra[i] + sa[i];
+                const uint64_t hb = __ballot(arr != 0) & hon_mask;   // receivers with arrivals
+                arr2 += arr;
+                st_cells += popc(hb);
+                // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
+                ob[i] = hb & ~__ballot((lo[i] & F_DEL) != 0);
+            }
+            st_arr += lane_in(hon_mask) ? arr2 : 0u;
+            if (!(ob[0] | ob[1])) return;                        // no open cell receives anything now
+            BRC_KCOUNT(3);
+            // Per-lane work below is branch-free integer arithmetic on 0/1 flags; a stage runs only
+            // when its message type can land (a stage without arrivals is the identity).
+            auto ge = [](uint32_t a, uint32_t b) -> uint32_t { return ((a - b) >> 31) ^ 1u; };   // a >= b (< 2^31)
+            uint32_t fl[2], ec[2], rc[2], es[2] = {0u, 0u}, rs[2] = {0u, 0u}, dl[2] = {0u, 0u};
+            bool opn[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                opn[i] = lane_in(ob[i]);
+                fl[i] = lo[i] & 31u; ec[i] = (lo[i] >> C32_EC_SH) & 63u; rc[i] = (lo[i] >> C32_RC_SH) & 63u;
+            }
+            if constexpr (BEB) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    dl[i] = (opn[i] && sa[i]) ? 1u : 0u;         // brb_cell_update_beb
+                    fl[i] |= dl[i] << 2;
+                }
+            } else if constexpr (SPEC) {
+                // brb_cell_update_spec: ECHO on the first SEND, one READY (echo quorum or f+1 READYs),
+                // DELIVER at 2f+1 READYs; only a growing set can newly pass a threshold
+                if (tbu & TB_S) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        es[i] = (opn[i] ? sa[i] : 0u) & ~(fl[i] >> 3) & 1u;   // !F_ES
+                        fl[i] |= es[i] << 3;
+                    }
+                }
+                if (tbu & (TB_E | TB_R)) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        ec[i] += opn[i] ? ea[i] : 0u;
+                        rc[i] += opn[i] ? ra[i] : 0u;
+                        rs[i] = (opn[i] ? 1u : 0u) & ~(fl[i] >> 4) & (ge(ec[i], T_echo) | ge(rc[i], T_amp));   // !F_RS
+                        fl[i] |= rs[i] << 4;
+                        dl[i] = (opn[i] ? 1u : 0u) & ge(rc[i], T_del);
+                        fl[i] |= dl[i] << 2;
+                    }
+                }
+            } else {
+                // brb_cell_update in integer form.  F_EEX = bit 0, F_REX = 1, F_DEL = 2, F_ES = 3, F_RS = 4.
+                if (tbu & TB_S) {                                                // :76-82
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        es[i] = (opn[i] ? sa[i] : 0u) & ~fl[i] & 1u;             // SEND, no ECHO entry
+                        fl[i] |= es[i] | (es[i] << 3);                           // F_EEX | F_ES
+                    }
+                }
+                if (tbu & TB_E) {                                                // :84-98
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const uint32_t e = opn[i] ? ea[i] : 0u;
+                        const uint32_t eon = min(e, 1u);
+                        const uint32_t chk = min(e + (fl[i] & 1u) - eon, 1u);    // a checked ECHO (:87-89)
+                        fl[i] |= eon;                                            // F_EEX
+                        ec[i] += e;
+                        const uint32_t r1 = eon & chk & ge(ec[i], T_echo) & (~fl[i] >> 1) & 1u;   // !F_REX (:95)
+                        fl[i] |= (r1 << 1) | (r1 << 4);                          // F_REX | F_RS
+                        rs[i] = r1;
+                    }
+                }
+                if (tbu & TB_R) {                                                // :100-119
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const uint32_t r = opn[i] ? ra[i] : 0u;
+                        const uint32_t ron = min(r, 1u);
+                        const uint32_t rexm = 0u - ((fl[i] >> 1) & 1u);          // all ones iff F_REX
+                        const uint32_t rlo = 2u + ((rc[i] - 1u) & rexm), rhi = r + (rc[i] & rexm);   // checked sizes
+                        fl[i] |= ron << 1;                                       // F_REX
+                        rc[i] += r;
+                        const uint32_t any = ron & ge(rhi, rlo);
+                        const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+                        const uint32_t r2 = any & ~fl[i] & ~(fl[i] >> 4) & ge(ahi, alo) & 1u;   // !F_EEX, !F_RS
+                        fl[i] |= r2 << 4;                                        // F_RS
+                        dl[i] = any & ge(rhi, T_del);
+                        fl[i] |= dl[i] << 2;                                     // F_DEL
+                        rs[i] |= r2;
+                    }
+                }
+            }
+            uint64_t eb[2], rb[2], db[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                // new word for open cells; the others keep theirs.  A count reaches 64 only when every
+                // sender's message of that type has arrived, so none is compared again: the stored
+                // counts saturate at 63 without changing any later transition
+                nw[i] = fl[i] | (min(ec[i], 63u) << C32_EC_SH) | (min(rc[i], 63u) << C32_RC_SH) |
+                        ((es[i] ? ts : tE[i]) << C32_OE_SH) | ((rs[i] ? ts : tR[i]) << C32_OR_SH);
+                wr[i] = opn[i];
+                eb[i] = __ballot(es[i] != 0); rb[i] = __ballot(rs[i] != 0); db[i] = __ballot(dl[i] != 0);
+            }
+            st_bcast += popc(eb[0]) + popc(rb[0]) + popc(eb[1]) + popc(rb[1]);
+            st_del += popc(db[0]) + popc(db[1]);
+            if (db[0] | db[1]) {
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (db[i]) {
+                        if constexpr (DBG) {
+                            // keys come in ascending slot order: a word is complete when the next word starts
+                            const uint32_t wk = k[i] >> 6;
+                            if (wk != dcur) {
+                                if (dcur != NOKEY) flush_dacc(dcur, dacc);
+                                dacc = 0; dcur = wk;
+                            }
+                            dacc |= (uint64_t)dl[i] << (k[i] & 63);
+                        } else {
+                            atomicOr((unsigned long long*)&s_dbits[(k[i] >> 6) * 64 + lane], (uint64_t)dl[i] << (k[i] & 63));
+                        }
+                    }
+                }
             }
             if (EV) {
-                const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
-                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
-                if (rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
-                if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const uint32_t kp = (k[i] >> qsh), s = m_s1(m[i]) - 1u;
+                    if (es[i]) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m[i]));
+                    if (rs[i]) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m[i]));
+                    if (dl[i]) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m[i]));
+                }
             }
-            // sends: ring marks at t + every delay some sending lane has; t_quiet of the key
-            const uint64_t sb = __ballot(es || rs);
-            if (sb) {
-                uint32_t os = 0;
+            // sends: typed ring marks at t + every delay some sending lane has (the step's ring rows,
+            // q_until and the keys' pending arrivals follow from the ring itself)
+            if (eb[0] | rb[0] | eb[1] | rb[1]) {
                 if constexpr (NLR != 0) {
-                    if (sb & OV0) os |= 1u << (dly0 - 1u);
-                    if (sb & OV1) os |= 1u << (dly1 - 1u);
+                    // one LDS op for the pair: lane L < 8 marks key L >> 2, type (L >> 1) & 1 (ECHO,
+                    // READY), delay class L & 1 -- iff a sender of that type has a link of that class
+                    const bool lk1 = lane_in(0xF0F0F0F0F0F0F0F0ull), lty = lane_in(0xCCCCCCCCCCCCCCCCull);
+                    const uint64_t sm = (lk1 ? (lty ? rb[1] : eb[1]) : (lty ? rb[0] : eb[0])) & mk_ov;
+                    const uint32_t kx = lk1 ? k[1] : k[0];
+                    if (lane < 8 && sm != 0) atomicOr((unsigned long long*)&s_act[mk_row + (kx >> 6)], 1ull << (kx & 63));
                 } else {
-                    for (uint32_t ds = dset; ds; ds &= ds - 1) {
-                        const uint32_t i = (uint32_t)__ffs(ds) - 1;
-                        if (sb & readlane64(outv, (int)i)) os |= 1u << i;
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        uint32_t osE = 0, osR = 0;
+                        for (uint32_t ds = dset; ds; ds &= ds - 1) {
+                            const uint32_t j = (uint32_t)__ffs(ds) - 1;
+                            const uint64_t ov = readlane64(outv, (int)j);
+                            if (eb[i] & ov) osE |= 1u << j;
+                            if (rb[i] & ov) osR |= 1u << j;
+                        }
+                        const uint64_t kbit = 1ull << (k[i] & 63);
+                        for (uint32_t x = osE | (osR << 16); x; x &= x - 1) {
+                            const uint32_t b = (uint32_t)__ffs(x) - 1;
+                            const uint32_t r = (t + (b & 15u) + 1u) & (RS - 1);
+                            if (lane == 0) atomicOr((unsigned long long*)&s_act[(r * AT + (b >> 4)) * nkw + (k[i] >> 6)], kbit);
+                        }
                     }
-                }
-                for (uint32_t x = os; x; x &= x - 1) {
-                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
-                    if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
-                    any_rows |= 1u << r;
-                }
-                const uint32_t myq = os ? t + hibit(os) : 0u;
-                if (myq) {
-                    if (myq > m_tquiet(m)) s_meta[k] = m_with_tquiet(m, myq);   // uniform: every lane writes it
-                    q_until = max(q_until, myq);
                 }
             }
         };
@@ -1161,7 +1271,7 @@ void brc_step(const Params* __restrict__ pp) {
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
-            auto cell = [&](uint32_t k) { return (ccells + (size_t)k * 64)[lane]; };
+            auto cell = [&](uint32_t e) { return (ccells + (size_t)(e & TB_KEY) * 64)[lane]; };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
             Unrolled<CHUNK>::run([&](auto ci) {
@@ -1174,28 +1284,28 @@ void brc_step(const Params* __restrict__ pp) {
                 uint64_t mm[CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    mm[c] = s_meta[kk[c]];
+                    mm[c] = s_meta[kk[c] & TB_KEY];
                 });
                 // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
                 // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own
                 static_assert(CHUNK == 4, "four u16 key ids per 8-B read");
                 const uint64_t knext = *(const uint64_t*)&s_klist[p + CHUNK];
-                Unrolled<CHUNK>::run([&](auto ci) {
-                    constexpr int c = decltype(ci)::value;
-                    // exactly one whole-wave store per slot (unchanged lanes write their word back,
-                    // slots past the list write the trash row): with a fixed count of memory
-                    // operations between a load and its use, the compiler waits for exactly that
-                    // load (vmcnt(CHUNK - 1)) instead of for the younger stores as well
-                    uint32_t nw = w[c];
-                    bool wr = false;
-                    if (p + c < nkeys) process_lean(kk[c], uni64(mm[c]), w[c], nw, wr);
-#ifdef BRC_WHOLE_STORE
-                    (ccells + (size_t)kk[c] * 64)[lane] = wr ? nw : w[c];
-#else
-                    if (wr) (ccells + (size_t)kk[c] * 64)[lane] = nw;
-#endif
+                Unrolled<CHUNK / 2>::run([&](auto ci) {
+                    constexpr int c = 2 * decltype(ci)::value;
+                    // a pair past the list is skipped; the second key of a pair at the list's end is
+                    // the padding entry (the trash row, no message type): it changes nothing
+                    const uint32_t ent[2] = {kk[c], kk[c + 1]};
+                    const uint64_t mp[2] = {uni64(mm[c]), uni64(mm[c + 1])};
+                    const uint32_t lo[2] = {w[c], w[c + 1]};
+                    uint32_t nw[2] = {w[c], w[c + 1]};
+                    bool wr[2] = {false, false};
+                    if (p + c < nkeys) process_pair(ent, mp, lo, nw, wr);
+                    if (wr[0]) (ccells + (size_t)(kk[c] & TB_KEY) * 64)[lane] = nw[0];
+                    if (wr[1]) (ccells + (size_t)(kk[c + 1] & TB_KEY) * 64)[lane] = nw[1];
                     kk[c] = (uint32_t)(uni64(knext) >> (16 * c)) & 0xFFFFu;
                     w[c] = cell(kk[c]);
+                    kk[c + 1] = (uint32_t)(uni64(knext) >> (16 * (c + 1))) & 0xFFFFu;
+                    w[c + 1] = cell(kk[c + 1]);
                 });
             }
         } else {
@@ -1217,8 +1327,20 @@ void brc_step(const Params* __restrict__ pp) {
                 });
             }
         }
-        if constexpr (DBG) {
-            if (dcur != NOKEY) { gdbits[dcur * 64] = dacc; dwm |= 1u << dcur; }
+        if constexpr (LEAN) {
+            if (dcur != NOKEY) flush_dacc(dcur, dacc);
+            // ring rows the key loop marked (every row but the current one, which it consumes), and
+            // q_until = the furthest of them: the same values per-key tracking would have produced
+            const uint32_t rsh = (uint32_t)__ffs(AT * nkw) - 1u;      // AT * nkw is a power of two
+            uint32_t rb = 0;
+            for (uint32_t i = lane; i < RS * AT * nkw; i += 64)
+                if (s_act[i] != 0) rb |= 1u << (i >> rsh);
+            rb = uni32(wave_or(rb)) & ~(1u << row);
+            if (rb) {
+                any_rows |= rb;
+                const uint32_t rel = (row ? ((rb >> row) | (rb << (RS - row))) : rb) & (RS == 32 ? ~0u : ((1u << RS) - 1u));
+                q_until = max(q_until, t + hibit(rel) - 1u);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(1);
@@ -1360,7 +1482,7 @@ void brc_step(const Params* __restrict__ pp) {
                 if (!pending) status = BRC_QUIESCENT;
             }
         }
-        if ((uint32_t)lane < nkw) s_act[row * nkw + lane] = 0;
+        if ((uint32_t)lane < nkw * AT) s_act[row * nkw * AT + lane] = 0;
         any_rows &= ~(1u << row);
         if constexpr (LEAN) {
             // The key loop's last refills load past the list (trash row) and nothing reads them;
@@ -1387,7 +1509,7 @@ void brc_step(const Params* __restrict__ pp) {
                 gp(P.mgen)[mb + i] = LEAN ? ((s_meta[i] & M_RESTRICTED) ? GEN_RESTRICTED : 0u) : gen32(s_gen[i]);
             }
         }
-        for (uint32_t i = lane; i < RS * nkw; i += 64) gp(P.act)[item * RS * nkw + i] = s_act[i];
+        for (uint32_t i = lane; i < RS * nkw * AT; i += 64) gp(P.act)[item * RS * nkw * AT + i] = s_act[i];
     }
     if (lane == 0) {
         gp(P.actany)[item] = any_rows;
@@ -1410,6 +1532,7 @@ void brc_step(const Params* __restrict__ pp) {
             for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
         }
     }
+    if (LEAN && lane != 0) { st_cells = 0; st_del = 0; st_bcast = 0; }   // lean: wave-uniform counts
     st_msgs += st_bcast * n;
     if (LEAN && real) st_loads += nk_lean - nk_skip;
     // statistics: reduce over the segment, its leader writes the instance row

@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="collective backend for N > 1: nccl (= RCCL over xGMI, one GPU per rank); gloo "
                          "only rehearses the multi-rank flow with several ranks sharing one GPU")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group (and run the statistics all-reduce) even at world size 1, "
+                         "e.g. one RCCL rank under torch.distributed.run --nproc-per-node 1")
     a = ap.parse_args()
     a.legs = [a.mode] if a.mode else [x for x in a.legs.split(",") if x]
     return a
@@ -99,10 +102,12 @@ def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
 
 
 def load_traffic(instances, kernel_ms, mode="reference"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json,
-    written by profiles/summarize.py), used only if it was taken on this workload and size and
-    its kernel time agrees with the live one within 15 % (i.e. the same kernel build)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json for
+    the reference leg, profiles/pmc_traffic_<mode>.json for the others, written by
+    profiles/summarize.py), used only if it was taken on this workload and size and its kernel time
+    agrees with the live one within 15 % (i.e. the same kernel build)."""
+    name = "pmc_traffic.json" if mode == "reference" else "pmc_traffic_%s.json" % mode
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as fh:
             d = json.load(fh)
@@ -195,23 +200,27 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     kernel_ms = shard.max_over_ranks(kernel_ms, dist, device=coll_dev)
     decided, arrivals, cell_steps = st["decided"], st["arrivals"], st["cell_steps"]
     bad = st["overflow"] + st["stepcap"] + st["running"]
-    if bad:
-        print("WARNING: %s leg: %d instances did not finish cleanly" % (mode, bad), file=sys.stderr)
+    if bad:      # a leg whose instances did not all finish measures nothing: fail the run
+        raise SystemExit("%s leg: %d instances did not finish cleanly (overflow %d, stepcap %d, running %d)"
+                         % (mode, bad, st["overflow"], st["stepcap"], st["running"]))
     launches = len(tiles)
     cs_gpu = cell_steps / world
-    achieved = SURVEY_BYTES_PER_CELL_STEP * cs_gpu / (kernel_ms / 1e3) / 1e9
-    floor = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / (kernel_ms / 1e3) / 1e9
+    secs = kernel_ms / 1e3
+    # algorithmic bytes of THIS layout: the 4-B cell word read + written per cell-step
+    achieved = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
+    survey = SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
     traffic = load_traffic(per, kernel_ms, mode) if launches == 1 else None
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_frac": (traffic / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
-            "floor_frac": floor / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
-            "note": "algorithmic = %d B (SURVEY 8(d)) x %d cell-steps per GPU per step (%d launch%s): it credits "
-                    "n-bit ECHO/READY masks this design never moves (one %d-B word per cell), so frac can pass 1; "
-                    "the physical figures are floor_frac (%d B: the cell word read + written, per cell-step) and "
-                    "traffic_frac (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch, profiles/pmc_traffic.json)"
-                    % (SURVEY_BYTES_PER_CELL_STEP, cs_gpu, launches, "" if launches == 1 else "es",
-                       CELL_BYTES, FLOOR_BYTES_PER_CELL_STEP)}
+            "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "survey_model_frac": survey / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
+            "bytes_per_unit": FLOOR_BYTES_PER_CELL_STEP, "units_per_launch": cs_gpu / launches,
+            "note": "achieved = %d B (the %d-B cell word read + written) x %d cell-steps per GPU per step (%d launch%s)"
+                    " / kernel time; traffic = rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch (profiles/"
+                    "pmc_traffic*.json); survey_model_frac prices SURVEY 8(d)'s %d B per cell-step, which credits "
+                    "n-bit ECHO/READY masks this design never moves, so it can pass 1"
+                    % (FLOOR_BYTES_PER_CELL_STEP, CELL_BYTES, cs_gpu, launches, "" if launches == 1 else "es",
+                       SURVEY_BYTES_PER_CELL_STEP)}
     leg = {
         "value": decided * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -239,7 +248,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     coll_dev = "cuda"
-    if world > 1:
+    if world > 1 or args.dist:
         import torch
         import torch.distributed as tdist
         if args.backend == "gloo":                  # rehearsal: ranks may share a GPU
@@ -268,12 +277,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u64",
+            "dtype": "u32",
             "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
             "config": {"workload": head["workload"], "n": N_REPLICAS, "f": F_FAULTS,
                        "instances_per_gpu": args.instances, "round_cap": args.round_cap, "mode": head_mode,
                        "key_window": 8 if head_mode == "spec" else 4,
                        "parallelism": "instance-sharded x%d" % world},
+            "collective": (dist.get_backend() + " all-reduce of the statistics") if dist is not None else None,
         }
         for k in ("kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
                   "agreement_violations", "replica_message_steps_per_s", "counts", "roofline"):

@@ -6,6 +6,7 @@ class keeps the reference's constructor, constants and methods and forwards to t
 ``network.Cluster``.  ``consensus_instance.deliver(payload)`` is called exactly as at :115.
 """
 from ..base.broadcast import Broadcast
+from .. import _lib as L
 from .. import network
 
 
@@ -30,7 +31,11 @@ class BRBroadcast(Broadcast):
         self.listening = True
 
     def _cluster_send(self, message_type, message):
-        if message_type != self.SEND:
-            # ECHO/READY are produced by the engine's handler itself (:82, :98, :119)
-            raise NotImplementedError("only SEND broadcasts can be issued from user code")
-        self.cluster.brb_send(self.node_id, message)
+        if message_type == self.SEND:
+            self.cluster.brb_send(self.node_id, message)
+        elif message_type in (self.ECHO, self.READY):
+            # user code may issue ECHO / READY itself (base/broadcast.py:17): every peer gets it
+            self.cluster.brb_msg(self.node_id, message_type, message)
+        else:
+            raise L.EngineError(L.E_UNSUPPORTED, "message type %r: the engine carries SEND, ECHO and READY"
+                                % (message_type,))

@@ -23,7 +23,10 @@ Deviations from the reference, all reported by exceptions and never silent:
   decided ``round_cap`` times (``configure``).
 * At most three distinct proposal strings besides ``"-1"`` (two-bit value ids).
 * A payload SENT by two different origins is one key in the reference (its dicts are keyed
-  by the payload string).  The engine models one sender per key and raises ``EngineError``.
+  by the payload string).  The engine models one sender per key and raises ``EngineError``
+  (also when another node first used the payload in an ECHO / READY broadcast).
+* ``broadcast(type, m)`` takes SEND, ECHO and READY (the reference also puts other types on
+  the wire, which its handler then ignores): other types raise ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
   (crashed) replicas.
 
@@ -143,6 +146,7 @@ class Cluster:
         self.payload_key = {}      # BRB payload -> (origin, seq)
         self.key_payload = {}      # (origin, seq) -> payload
         self.seq = {}
+        self.sent = set()          # keys SENT (a payload may be declared first by an ECHO / READY)
         self.values = ValueTable()
         self.engine = None
         self.seen_events = 0
@@ -193,22 +197,46 @@ class Cluster:
         return not self.finished and bool(self.actions)
 
     # ------------------------------------------------------------------ actions
+    def _key_of(self, i, payload):
+        """The payload's key; a payload new to the cluster gets the key (i, i's next sequence
+        number).  The reference keys its dicts by the payload string (core/brbroadcast.py:38-44)."""
+        key = self.payload_key.get(payload)
+        if key is None:
+            s = self.seq.get(i, 0)
+            self.seq[i] = s + 1
+            key = (i, s)
+            self.payload_key[payload] = key
+            self.key_payload[key] = payload
+        return key
+
     def brb_send(self, i, payload):
         """BRBroadcast.broadcast(SEND, payload) by replica i (base/broadcast.py:17-40)."""
         if self.cons:
             raise L.EngineError(L.E_UNSUPPORTED, "raw BRB SENDs on a consensus cluster")
         payload = str(payload)
-        key = self.payload_key.get(payload)
-        if key is not None:
-            if key[0] == i:
-                return            # identical message on the same links: suppressed
+        key = self._key_of(i, payload)
+        if key[0] != i:
             raise L.EngineError(L.E_UNSUPPORTED, "payload %r SENT by two origins (one reference key)" % payload)
-        s = self.seq.get(i, 0)
-        self.seq[i] = s + 1
-        self.payload_key[payload] = (i, s)
-        self.key_payload[(i, s)] = payload
-        self.actions.append(dict(t=self.t, kind=L.INJ_SEND, node=i, kp=i, s=s, value=0,
+        if key in self.sent:
+            return                # identical message on the same links: suppressed
+        self.sent.add(key)
+        self.actions.append(dict(t=self.t, kind=L.INJ_SEND, node=i, kp=i, s=key[1], value=0,
                                  dst=(1 << len(self.peers)) - 1))
+
+    def brb_msg(self, i, message_type, payload):
+        """BRBroadcast.broadcast(ECHO | READY, payload) issued by replica i's own code
+        (base/broadcast.py:17 accepts any type): the message goes to every peer, self included,
+        exactly as the handler's own ECHO / READY broadcasts do (core/brbroadcast.py:82, :98,
+        :119).  A payload nobody has SENT gets a key of its own (declared, never SENT)."""
+        if self.cons:
+            raise L.EngineError(L.E_UNSUPPORTED, "raw BRB messages on a consensus cluster")
+        payload = str(payload)
+        new = payload not in self.payload_key
+        key = self._key_of(i, payload)
+        if new:
+            self.actions.append(dict(t=self.t, kind=L.INJ_KEY, node=i, kp=i, s=key[1], value=0))
+        self.actions.append(dict(t=self.t, kind=L.INJ_MSG, type=message_type, node=i, kp=key[0], s=key[1],
+                                 value=0, dst=(1 << len(self.peers)) - 1))
 
     def propose(self, i, message):
         """ByzantineRandomizedConsensus.propose (core/byzantinerandomizedconsensus.py:43-50)."""

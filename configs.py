@@ -18,8 +18,9 @@ Workloads:
   cfg5-*     n=256 f=85 SPEC, 2048 instances per GPU, const / uniform[1,4] / geometric<=16
 
 A step is one pass of the hot path over the batch (reset + run to completion); the timed region
-is K steps between barriers, max over ranks.  `roofline.achieved` = SURVEY §8(d)'s algorithmic
-6*ceil(n/8)+2 B per cell-step x cell-steps per launch / kernel time.
+is K steps between barriers, max over ranks.  `roofline.achieved` = this layout's algorithmic
+bytes (the cell word read + written, 2 x cell bytes per cell-step) x cell-steps per launch /
+kernel time; `survey_model_frac` prices SURVEY §8(d)'s 6*ceil(n/8)+2 B per cell-step instead.
 """
 import argparse
 import json
@@ -97,18 +98,19 @@ def measured_traffic(name, kernel_ms):
 
 
 def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0):
-    """Algorithmic, floor (this layout's cell word read + written per cell-step)
-    and counter-measured HBM fractions of the dominant kernel, as bench.py reports them."""
+    """HBM fractions of the dominant kernel, as bench.py reports them: `frac` prices this layout's
+    algorithmic bytes (the cell word read + written per cell-step), `survey_model_frac` SURVEY
+    §8(d)'s n-bit-mask model, `traffic_frac` the rocprofv3 counters of a committed profile."""
     sec = kernel_ms / 1e3
     floor_b = 2 * cell_bytes(n, peer_mode)
-    achieved = bpc * cell_steps / sec / 1e9
+    achieved = floor_b * cell_steps / sec / 1e9
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": achieved,
-           "frac": achieved / HBM_PEAK_GBS,
-           "floor_frac": floor_b * cell_steps / sec / 1e9 / HBM_PEAK_GBS, "cell_bytes": floor_b // 2,
+           "frac": achieved / HBM_PEAK_GBS, "bytes_per_unit": floor_b,
+           "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS, "cell_bytes": floor_b // 2,
            "traffic": None, "traffic_frac": None,
-           "note": "algorithmic %d B per cell-step (SURVEY 8(d) at n=%d) credits n-bit sets this layout never "
-                   "moves, so frac can pass 1; floor_frac: %d B per cell-step; traffic_frac: rocprofv3 "
-                   "FETCH_SIZE x 2 + WRITE_SIZE" % (bpc, n, floor_b)}
+           "note": "achieved: %d B per cell-step (the %d-B cell read + written); survey_model_frac prices SURVEY "
+                   "8(d)'s %d B at n=%d, which credits n-bit sets this layout never moves, so it can pass 1; "
+                   "traffic_frac: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE" % (floor_b, floor_b // 2, bpc, n)}
     t = measured_traffic(name, kernel_ms)
     if t:
         out["traffic"], out["traffic_source"] = t

@@ -79,10 +79,32 @@ def philox(ctr, key):
     return tuple(out)
 
 
+def expand_actions(actions, n):
+    """Harness actions with every "brb_msg" (an honest node's own ECHO / READY broadcast,
+    base/broadcast.py:17) restated as the raw message it puts on every link: a key declaration on
+    the payload's first use ("byz_key") and a "byz" message from the node to all peers.  Stable in
+    time order; the list order within a step is kept."""
+    declared = set()
+    out = []
+    for a in sorted(actions, key=lambda a: a["t"]):
+        if a["kind"] in ("brb_send", "byz_key"):
+            declared.add((a["kp"], a["s"]))
+        if a["kind"] != "brb_msg":
+            out.append(a)
+            continue
+        key = (a["kp"], a["s"])
+        if key not in declared:
+            declared.add(key)
+            out.append(dict(t=a["t"], kind="byz_key", kp=a["kp"], s=a["s"], value=a.get("value", 0)))
+        out.append(dict(t=a["t"], kind="byz", src=a["node"], type=a["type"], kp=a["kp"], s=a["s"],
+                        dst=(1 << n) - 1))
+    return out
+
+
 def run(spec, light=False):
     """Run one instance of ``spec`` (harness format) and return the harness result format.
     ``light``: status and counters only (no event lists; one C call, no Python conversion)."""
-    acts = sorted(spec.get("actions", []), key=lambda a: a["t"])
+    acts = expand_actions(spec.get("actions", []), spec["n"])
     arr = (_Action * max(1, len(acts)))()
     for i, a in enumerate(acts):
         x = arr[i]

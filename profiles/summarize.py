@@ -5,7 +5,8 @@
 
 Writes <dest>/kernel_stats.csv (the rocprofv3 --stats table, copied), <dest>/pmc_summary.json
 (per-kernel mean of every PMC counter over its dispatches) and, for the headline kernel,
-profiles/pmc_traffic.json, which bench.py reads for roofline.traffic.
+profiles/pmc_traffic.json (profiles/pmc_traffic_spec.json for the SPEC leg), which bench.py
+reads for roofline.traffic.
 
 HBM bytes follow MI355X_MICROARCH.md (rocprofv3 / HBM section): FETCH_SIZE and WRITE_SIZE are
 in KiB and come from separate --pmc passes; on gfx950 FETCH_SIZE reports half the bytes of a
@@ -78,10 +79,12 @@ def main():
         out["mode"] = cfg.get("mode", "reference")
         out["bench_kernel_ms"] = bench.get("kernel_ms")
         out["cell_bytes"] = bench.get("roofline", {}).get("cell_bytes", 8)
-    # the bench reads profiles/pmc_traffic.json for its headline (reference) leg only
+    # the bench reads profiles/pmc_traffic.json for its reference leg, pmc_traffic_<mode>.json for the others
     paths = [os.path.join(dest, "pmc_traffic.json")]
-    if out.get("mode", "reference") == "reference" and out.get("headline", True):
-        paths.append(os.path.join(os.path.dirname(dest.rstrip("/")), "pmc_traffic.json"))
+    if out.get("headline", True):
+        mode = out.get("mode", "reference")
+        name = "pmc_traffic.json" if mode == "reference" else "pmc_traffic_%s.json" % mode
+        paths.append(os.path.join(os.path.dirname(dest.rstrip("/")), name))
     for path in paths:
         with open(path, "w") as fh:
             json.dump(out, fh, indent=1, sort_keys=True)

@@ -8,6 +8,7 @@ from collections import defaultdict
 
 from byzantinerandomizedconsensus_amd import _lib as L
 from byzantinerandomizedconsensus_amd.engine import Engine
+from oracle.oracle import expand_actions
 
 KIND = {"propose": L.INJ_PROPOSE, "brb_send": L.INJ_SEND, "byz_key": L.INJ_KEY}
 
@@ -31,7 +32,7 @@ def _injections(sp, local):
     allm = (1 << n) - 1
     values = {}
     out = []
-    for a in sorted(sp.get("actions", []), key=lambda a: a["t"]):
+    for a in expand_actions(sp.get("actions", []), n):
         k = a["kind"]
         if k == "propose":
             out.append(dict(t=a["t"], kind=L.INJ_PROPOSE, instance=local, node=a["node"], value=a["value"]))

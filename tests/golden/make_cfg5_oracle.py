@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 N, F, SEED, COIN, COUNT = 256, 85, 0x5EED0005, 0xC017C017, 512
 MODELS = [(0, 1), (1, 4), (3, 16)]          # const D=1, uniform [1,4], geometric cap 16 (configs.py cfg5)
-PER_MODEL = 4
+PER_MODEL = 16
 
 
 def sample_ids(model):

@@ -330,6 +330,9 @@ class Run:
             key = (a["kp"], a["s"])
             self.register(a["payload"], key)
             self.nodes[a["node"]].broadcast(SEND, a["payload"])   # base/broadcast.py:17
+        elif kind == "brb_msg":       # an honest node's user code broadcasts ECHO / READY
+            self.register(a["payload"], (a["kp"], a["s"]))
+            self.nodes[a["node"]].broadcast(a["type"], a["payload"])   # base/broadcast.py:17
         elif kind == "byz_key":       # declare a Byzantine key and its payload
             key = (a["kp"], a["s"])
             if self.mode == "consensus":

@@ -12,6 +12,9 @@ actions (each performed after step ``t`` is processed, messages stamped ``t``):
     {"kind": "brb_send", "t", "node", "kp", "s", "payload"}     BRBroadcast.broadcast(SEND, payload)
     {"kind": "byz_key",  "t", "kp", "s", "value"[, "payload"]}   declare a Byzantine key
     {"kind": "byz",      "t", "src", "type", "kp", "s", "dst"}   raw Byzantine message(s)
+    {"kind": "brb_msg",  "t", "node", "type", "kp", "s", "payload"}
+                                      an honest node's own BRBroadcast.broadcast(ECHO | READY, payload)
+                                      (base/broadcast.py:17): the key is declared on first use
 """
 import copy
 import random
@@ -80,6 +83,21 @@ def beb_cons_spec(n, f, seed, model, dmax, g, round_cap=1, **kw):
     sp = cons_spec(n, f, seed, model, dmax, g, round_cap=round_cap, **kw)
     sp.update(mode="beb_consensus")
     return sp
+
+
+def user_msg_actions():
+    """Honest nodes issue ECHO / READY broadcasts from user code (base/broadcast.py:17 accepts any
+    type): an early ECHO of a SENT payload, an ECHO of a payload nobody SENDs, READYs of a fresh
+    payload from f + 1 nodes (amplification, then delivery without any SEND), and a READY of a SENT
+    payload.  Keys follow the class API's allocation: a payload's key is (first user, that node's
+    next sequence number)."""
+    E, R = ECHO, READY
+    return [dict(t=0, kind="brb_msg", node=5, type=E, kp=0, s=0, payload="TEST 1.0"),
+            dict(t=0, kind="brb_msg", node=4, type=E, kp=4, s=0, payload="USER E"),
+            dict(t=0, kind="brb_msg", node=4, type=R, kp=4, s=1, payload="USER R"),
+            dict(t=0, kind="brb_msg", node=5, type=R, kp=4, s=1, payload="USER R"),
+            dict(t=0, kind="brb_msg", node=6, type=R, kp=4, s=1, payload="USER R"),
+            dict(t=0, kind="brb_msg", node=6, type=R, kp=1, s=0, payload="TEST 2.0")]
 
 
 def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
@@ -262,6 +280,11 @@ def scenario_groups():
                                       extra=deliver_actions(6, 0xDE10 + g)) for (m, d) in ((0, 1), (1, 3)) for g in range(3)]
     G["cons_deliver_n16"] = [cons_spec(16, 3, 0xDE20, 2, 4, g, round_cap=1, extra=deliver_actions(16, 0xDE20 + g))
                              for g in range(2)]
+    # ECHO / READY broadcasts issued by honest nodes' user code (base/broadcast.py:17), both peer modes
+    G["brb_usermsg_n7"] = [brb_spec(7, 2, 0x05E1, m, d, g, [(0, i, 0) for i in range(4)], extra=user_msg_actions())
+                           for (m, d) in ((0, 1), (1, 3)) for g in range(3)]
+    G["conn_brb_usermsg_n7"] = [clone(sp, peer_mode="connection", name="conn_brb_usermsg_n7/%d" % i)
+                                for i, sp in enumerate(G["brb_usermsg_n7"])]
     # the reference's own drivers (test/brb_test.py, test/brc_test.py) as they run: connection peers
     G["conn_brb_fifo_n4"] = [clone(G["brb_fifo_n4"][0], peer_mode="connection", name="conn_brb_fifo_n4/0")]
     G["conn_cons_brc_test_n6"] = [clone(G["cons_brc_test_n6"][0], peer_mode="connection",

@@ -90,8 +90,19 @@ def test_brb_sends_become_injections():
     assert c.key_payload == {(2, 0): "A", (2, 1): "B"}
     with pytest.raises(L.EngineError):
         nodes[1].broadcast(BRBroadcast.SEND, "A")  # one reference key, two origins
-    with pytest.raises(NotImplementedError):
-        nodes[1].broadcast(BRBroadcast.ECHO, "A")
+    # user-issued ECHO / READY (base/broadcast.py:17): the payload's key, every peer addressed;
+    # a payload nobody SENT is declared first under the caller's next sequence number
+    nodes[1].broadcast(BRBroadcast.ECHO, "A")
+    nodes[3].broadcast(BRBroadcast.READY, "C")
+    nodes[3].broadcast(BRBroadcast.SEND, "C")
+    acts = [(a["kind"], a.get("type", 0), a["node"], a["kp"], a["s"]) for a in c.actions[2:]]
+    assert acts == [(L.INJ_MSG, BRBroadcast.ECHO, 1, 2, 0), (L.INJ_KEY, 0, 3, 3, 0),
+                    (L.INJ_MSG, BRBroadcast.READY, 3, 3, 0), (L.INJ_SEND, 0, 3, 3, 0)]
+    assert all(a["dst"] == 15 for a in c.actions if a["kind"] != L.INJ_KEY)
+    with pytest.raises(L.EngineError):
+        nodes[0].broadcast(BRBroadcast.SEND, "C")  # declared by node 3
+    with pytest.raises(L.EngineError):
+        nodes[0].broadcast(7, "D")                 # the engine carries SEND / ECHO / READY only
     with pytest.raises(ValueError):
         BRBroadcast(4, 1, ("localhost", 1), peers, None)
 
@@ -246,3 +257,40 @@ def test_direct_deliver_calls_match_oracle():
                                                  "message": S.VALUES[a["value"]]}))
         cluster.run()
         assert got == [[t, node, v] for (t, node, _r, v) in sorted(exp["events"]["decide"])], g
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("group", ["brb_usermsg_n7", "conn_brb_usermsg_n7"])
+def test_user_echo_ready_broadcasts_match_reference(group):
+    """Honest nodes' user code issues ECHO / READY broadcasts (base/broadcast.py:17): an early ECHO
+    of a SENT payload, ECHO / READY of payloads nobody SENDs (f + 1 READYs -> amplification ->
+    delivery without a SEND), a READY that blocks a node's own (K3).  Upcalls at the steps and in
+    the order the reference issued them, in both peer modes."""
+    from byzantinerandomizedconsensus_amd.base.broadcast import IBroadcastHandler
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    for case in GROUPS[group]:
+        sp = case["spec"]
+        network.reset()
+        network.configure(delay_model=sp["delay_model"], delay_max=sp["dmax"], seed=sp["seed"],
+                          instance_id=sp["g"], peer_mode=sp.get("peer_mode", "sender"))
+        got = []
+
+        class H(IBroadcastHandler):
+            def __init__(self, i):
+                self.i = i
+
+            def deliver(self, message):
+                got.append([cluster.t, self.i, message])
+
+        peers = _peers(sp["n"], 6700)
+        nodes = [BRBroadcast(sp["n"], sp["f"], p, peers, H(i)) for i, p in enumerate(peers)]
+        cluster = nodes[0].cluster
+        payload = {}
+        for a in sp["actions"]:
+            assert a["t"] == 0
+            payload[(a["kp"], a["s"])] = a["payload"]
+            nodes[a["node"]].broadcast(BRBroadcast.SEND if a["kind"] == "brb_send" else a["type"], a["payload"])
+        assert {v: k for k, v in payload.items()} == cluster.payload_key     # the spec's keys are the API's
+        cluster.run()
+        exp = [[t, node, payload[(kp, s)]] for (t, node, kp, s) in case["result"]["raw_order"]["deliver"]]
+        assert got == exp, sp["name"]

@@ -9,7 +9,7 @@ cfg3: one rank's shard of the 1M-instance n=16 f=5 run: 125,000 instances at glo
       3 x 125,000, Byzantine {11..15} equivocating.
 cfg4: the bench batch, 131,072 instances n=64 f=21, slow-set delays D=8 (reference and SPEC).
 cfg4 at 2^20: the bench batch itself (reference protocol), 25 ids sampled across the range.
-cfg5: n=256 f=85, 512 instances per delay model (SPEC), 4 oracle-sampled ids per model.
+cfg5: n=256 f=85, 512 instances per delay model (SPEC), 16 oracle-sampled ids per model.
 """
 import hashlib
 import random
@@ -60,12 +60,13 @@ def _check_sample(res, reps, kw, base, ids, make_spec):
         if i in reps:
             first = {}
             for t, node, rnd, val in sorted(exp["events"]["decide"]):
-                first.setdefault(node, (rnd, t))
+                first.setdefault(node, (rnd, t, val))
             for d, rep in enumerate(reps[i]):
                 if d in sp.get("byzantine", []):
                     continue
                 if d in first:
-                    assert (rep["first_decide_round"], rep["first_decide_t"]) == first[d], (base + i, d)
+                    got = (rep["first_decide_round"], rep["first_decide_t"], rep["first_decide_value"])
+                    assert got == first[d], (base + i, d, got, first[d])
                 else:
                     assert rep["decide_count"] == 0, (base + i, d)
 
@@ -133,8 +134,9 @@ def test_cfg4_bench_batch_full_size(mode):
             assert sub[j][k] == exp[k], (g, k)
         first = {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
-            first.setdefault(node, rnd)
-        assert [r["first_decide_round"] for r in reps[j]] == [first[d] for d in range(64)]
+            first.setdefault(node, (rnd, t, val))
+        got = [(r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) for r in reps[j]]
+        assert got == [first[d] for d in range(64)], g
 
 
 def _cfg5_cases():
@@ -170,7 +172,8 @@ def test_cfg5_n256_full_size(model, dmax):
             assert res[g][k] == c[k], (model, g, k)
         for d, (rep, exp) in enumerate(zip(reps[g], c["first_decide"])):
             assert exp is not None, (g, d)
-            assert (rep["first_decide_round"], rep["first_decide_t"]) == (exp[0], exp[1]), (model, g, d)
+            got = (rep["first_decide_round"], rep["first_decide_t"], rep["first_decide_value"])
+            assert got == tuple(exp), (model, g, d)
 
 
 @pytest.mark.parametrize("mode", ["reference", "spec"])
@@ -188,9 +191,13 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
         hist = eng.round_histogram(66)
+        vals, disagreements = eng.decisions()
         res = {i: eng.instances_result(i, 1)[0] for i in ids}
         reps = {i: eng.replicas(i, 1)[0] for i in ids}
     assert hist[0] == 0 and sum(hist) == N, "every instance decided"
+    assert disagreements == 0 and vals["undecided"] == 0
+    assert sum(vals.values()) == N * 64, "one first decision per honest replica"
+    sampled = {}
     for g in ids:
         if spec:
             exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1, window=8, coin_seed=0xC017C017))
@@ -200,5 +207,55 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
             assert res[g][k] == exp[k], (g, k)
         first = {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
-            first.setdefault(node, (rnd, t))
-        assert [(r["first_decide_round"], r["first_decide_t"]) for r in reps[g]] == [first[d] for d in range(64)], g
+            first.setdefault(node, (rnd, t, val))
+        got = [(r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) for r in reps[g]]
+        assert got == [first[d] for d in range(64)], g
+        for d in range(64):
+            sampled[first[d][2]] = sampled.get(first[d][2], 0) + 1
+    # the decided-value histogram the bench reports: every sampled value occurs in it, and in SPEC
+    # mode (coin rounds) both binary values appear, in the reference protocol "-1" (id 0)
+    names = {0: "-1", 1: "0", 2: "1", 3: "3"}
+    for v in sampled:
+        assert vals[names[v]] > 0, (v, vals)
+    if spec:
+        assert vals["0"] > 0 and vals["1"] > 0 and vals["-1"] == 0
+    else:
+        assert vals["-1"] == N * 64, vals
+
+
+@pytest.mark.parametrize("mode", ["reference", "spec"])
+def test_cfg4_long_consensus_many_rounds(mode):
+    """Long-running consensus at scale (the reference re-proposes forever,
+    core/byzantinerandomizedconsensus.py:96-106): 2^17 cfg4 instances run to round_cap = 8
+    decisions per replica, so slots recycle and the compact cells' epoch moves across many rounds
+    under a full batch.  Sampled instances equal the oracle (counters and every replica's first
+    and last decision, values included)."""
+    L = _L()
+    N, CAP = 1 << 17, 8
+    spec = mode == "spec"
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=CAP, step_cap=4000, key_window=8 if spec else 4, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    ids = sorted(random.Random(8).sample(range(N), 6)) + [N - 1]
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        res_all = eng.instances_result()
+        res = {i: res_all[i] for i in ids}
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    assert all(r["status"] == "done" for r in res_all)
+    for g in ids:
+        if spec:
+            exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8,
+                                              coin_seed=0xC017C017))
+        else:
+            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP))
+        for k in KEYS:
+            assert res[g][k] == exp[k], (g, k)
+        first, last, count = {}, {}, {}
+        for t, node, rnd, val in sorted(exp["events"]["decide"]):
+            first.setdefault(node, (rnd, t, val))
+            last[node] = val
+            count[node] = count.get(node, 0) + 1
+        for d, r in enumerate(reps[g]):
+            assert (r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) == first[d], (g, d)
+            assert r["last_decide_value"] == last[d] and r["decide_count"] == count[d] >= CAP, (g, d)

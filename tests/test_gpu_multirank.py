@@ -64,3 +64,23 @@ def test_two_ranks_equal_one_rank_over_the_same_global_ids():
         assert m[leg]["counts"]["instances"] == PER_RANK * WORLD
         assert m[leg]["counts"]["decided"] > 0
         assert m[leg] == s[leg], leg
+
+
+@pytest.mark.gpu
+def test_rccl_rank_equals_plain_run():
+    """One rank under torch.distributed.run with the nccl backend (= RCCL on ROCm), process group
+    bound to the GPU (`device_id`): the statistics go through the device all-reduce of
+    `shard.reduce_stats` / `max_over_ranks` -- the 8-GPU path's collective, run on the one leased
+    GPU -- and must equal the plain single-process run over the same global ids."""
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec",
+                  "--instances", str(PER_RANK * WORLD)]
+    rccl = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                 "--gpus", "1", "--backend", "nccl", "--dist"] + bench_args, 300)
+    single = _run([sys.executable, "bench.py"] + bench_args, 300)
+    assert rccl["collective"] == "nccl all-reduce of the statistics"
+    assert single["collective"] is None
+    r, s = _legs(rccl), _legs(single)
+    for leg in ("reference", "spec"):
+        assert r[leg]["counts"]["decided"] > 0
+        assert r[leg] == s[leg], leg

@@ -45,9 +45,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
-    ap.add_argument("--legs", default="reference,spec",
-                    help="comma list of reference (the headline value) and spec (SURVEY §8 F3 coin rounds)")
-    ap.add_argument("--mode", choices=("reference", "spec"), default=None,
+    ap.add_argument("--legs", default="reference,spec,conn",
+                    help="comma list of reference (the headline value), spec (SURVEY §8 F3 coin rounds) and conn "
+                         "(connection-identity peers, what the shipped reference runs: SURVEY §8 F1)")
+    ap.add_argument("--mode", choices=("reference", "spec", "conn"), default=None,
                     help="shorthand for --legs <mode> (the headline leg is the first one run)")
     ap.add_argument("--round-cap", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
@@ -76,7 +77,8 @@ def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
         if mode == "spec":
             return S.spec_cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, g, round_cap=round_cap,
                                     window=window, coin_seed=COIN_SEED)
-        return S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, g, round_cap=round_cap)
+        return S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, g, round_cap=round_cap,
+                           peer_mode="connection" if mode == "conn" else "sender")
 
     t0 = time.perf_counter()
 
@@ -129,7 +131,7 @@ def make_engine(mode, count, first, device, round_cap):
                   delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=round_cap, step_cap=4000,
                   key_window=8 if spec else 4, variants=1, proposals=L.PROPOSALS_PHILOX,
                   instance_offset=first, device=device, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
-                  coin_seed=COIN_SEED)
+                  coin_seed=COIN_SEED, peer_mode=L.PEER_CONNECTION if mode == "conn" else L.PEER_SENDER)
 
 
 def collect(eng):
@@ -174,7 +176,10 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
             eng.reset_at(off)
             eng.run()
             kms += eng.last_kernel_ms()
+            kern.add(eng.last_kernel())
         return kms
+
+    kern = set()
 
     for _ in range(args.warmup):
         one_step()
@@ -195,6 +200,7 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
             eng.run()
             acc = add_stats(acc, collect(eng))
     eng.close()
+    kernel = kern.pop() if len(kern) == 1 else "mixed"
     st, hist = shard.reduce_stats(acc[0], dist, device=coll_dev, hist=acc[1])
     elapsed = shard.max_over_ranks(elapsed, dist, device=coll_dev)
     kernel_ms = shard.max_over_ranks(kernel_ms, dist, device=coll_dev)
@@ -206,21 +212,33 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     launches = len(tiles)
     cs_gpu = cell_steps / world
     secs = kernel_ms / 1e3
-    # algorithmic bytes of THIS layout: the 4-B cell word read + written per cell-step
-    achieved = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
-    survey = SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
     traffic = load_traffic(per, kernel_ms, mode) if launches == 1 else None
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
-            "survey_model_frac": survey / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
-            "bytes_per_unit": FLOOR_BYTES_PER_CELL_STEP, "units_per_launch": cs_gpu / launches,
-            "note": "achieved = %d B (the %d-B cell word read + written) x %d cell-steps per GPU per step (%d launch%s)"
-                    " / kernel time; traffic = rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch (profiles/"
-                    "pmc_traffic*.json); survey_model_frac prices SURVEY 8(d)'s %d B per cell-step, which credits "
-                    "n-bit ECHO/READY masks this design never moves, so it can pass 1"
-                    % (FLOOR_BYTES_PER_CELL_STEP, CELL_BYTES, cs_gpu, launches, "" if launches == 1 else "es",
-                       SURVEY_BYTES_PER_CELL_STEP)}
+    if kernel != "step":
+        # the key-lifetime kernel (csrc/brc_life.h) keeps a key's cells in registers for its whole
+        # lifetime: no cell bytes move, HBM carries only the per-instance results
+        roof = {"bound": "issue", "kernel": "brc_life", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": None, "traffic": traffic,
+                "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                "survey_model_frac": SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9 / HBM_PEAK_GBS,
+                "cell_steps_per_s": cs_gpu / secs,
+                "note": "no HBM cell traffic (cells stay in registers for a key's lifetime): bound by instruction "
+                        "issue, not HBM; survey_model_frac prices SURVEY 8(d)'s %d B per cell-step"
+                        % SURVEY_BYTES_PER_CELL_STEP}
+    else:
+        # algorithmic bytes of THIS layout: the 4-B cell word read + written per cell-step
+        achieved = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
+        survey = SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
+        roof = {"bound": "hbm", "kernel": "brc_step", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
+                "survey_model_frac": survey / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
+                "bytes_per_unit": FLOOR_BYTES_PER_CELL_STEP, "units_per_launch": cs_gpu / launches,
+                "note": "achieved = %d B (the %d-B cell word read + written) x %d cell-steps per GPU per step (%d "
+                        "launch%s) / kernel time; traffic = rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch "
+                        "(profiles/pmc_traffic*.json); survey_model_frac prices SURVEY 8(d)'s %d B per cell-step, which "
+                        "credits n-bit ECHO/READY masks this design never moves, so it can pass 1"
+                        % (FLOOR_BYTES_PER_CELL_STEP, CELL_BYTES, cs_gpu, launches, "" if launches == 1 else "es",
+                           SURVEY_BYTES_PER_CELL_STEP)}
     leg = {
         "value": decided * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -234,8 +252,11 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
         "counts": {k: st[k] for k in ("instances", "decided", "msgs_sent", "arrivals", "cell_steps", "deliveries",
                                       "decide_rounds_sum", "lane_loads", "max_t")},
         "roofline": roof,
+        "kernel": kernel,
         "workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
-                    % ("SPEC-protocol (common coin, phase window 8)" if mode == "spec" else "reference-protocol",
+                    % ({"spec": "SPEC-protocol (common coin, phase window 8)",
+                        "conn": "reference-protocol, connection-identity peers (core/brbroadcast.py:69),"}.get(
+                        mode, "reference-protocol"),
                        "first decision" if args.round_cap == 1 else "%d decisions" % args.round_cap, per),
     }
     return leg
@@ -282,10 +303,11 @@ def main():
             "config": {"workload": head["workload"], "n": N_REPLICAS, "f": F_FAULTS,
                        "instances_per_gpu": args.instances, "round_cap": args.round_cap, "mode": head_mode,
                        "key_window": 8 if head_mode == "spec" else 4,
+                       "peer_mode": "connection" if head_mode == "conn" else "sender",
                        "parallelism": "instance-sharded x%d" % world},
             "collective": (dist.get_backend() + " all-reduce of the statistics") if dist is not None else None,
         }
-        for k in ("kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
+        for k in ("kernel", "kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
                   "agreement_violations", "replica_message_steps_per_s", "counts", "roofline"):
             out[k] = head[k]
         for mode, leg in legs.items():

@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
 LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 OK, E_INVALID, E_NOMEM, E_HIP, E_UNSUPPORTED, E_STATE = 0, -1, -2, -3, -4, -5
 ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP error",
@@ -28,11 +28,12 @@ RUNNING, DONE, QUIESCENT, STEPCAP, OVERFLOW, BADINJ = 0, 1, 2, 3, 4, 5
 STATUS_NAMES = {RUNNING: "running", DONE: "done", QUIESCENT: "quiescent", STEPCAP: "stepcap",
                 OVERFLOW: "overflow", BADINJ: "bad_injection"}
 EV_DELIVER, EV_DECIDE, EV_SEND = 1, 2, 3
+KERNEL_STEP, KERNEL_LIFE = 0, 1
 
 EXPORTS = ["brc_create", "brc_load_proposals", "brc_load_byzantine", "brc_inject", "brc_run",
            "brc_reset", "brc_read_instances", "brc_read_replicas", "brc_read_events",
            "brc_read_stats", "brc_read_round_histogram", "brc_read_decisions", "brc_reset_at",
-           "brc_read_events_range", "brc_last_kernel_ms", "brc_device_count", "brc_last_error",
+           "brc_read_events_range", "brc_last_kernel_ms", "brc_last_kernel", "brc_device_count", "brc_last_error",
            "brc_destroy", "brc_abi_version"]
 
 
@@ -126,6 +127,7 @@ def load():
         "brc_read_events_range": ([vp, ctypes.c_size_t, ctypes.POINTER(Event), ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "brc_last_kernel_ms": ([vp, ctypes.POINTER(ctypes.c_float)], ctypes.c_int),
+        "brc_last_kernel": ([vp, ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
         "brc_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
         "brc_last_error": ([vp], ctypes.c_char_p),
         "brc_destroy": ([vp], None),

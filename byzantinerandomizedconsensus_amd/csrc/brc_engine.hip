@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -173,6 +174,12 @@ struct Engine {
     // per epoch (brc_reset to brc_reset); gen_base sums the epochs since the last full clear
     uint64_t gen_base = 0, gen_cur = 0;
     std::vector<std::pair<uint64_t, uint32_t>> send_keys;   // (instance, kp<<16|s) of injected SENDs
+    // key-lifetime kernel (brc_life.h): eligible configuration, engine fresh since create / reset,
+    // and whether the last run used it (its instances are then final: no re-opening injections)
+    bool life_cfg = false, fresh = true, life_done = false, last_life = false;
+    bool cells_ready = false;                    // the step kernel's cell array (allocated on first use
+                                                 // when the lifetime kernel may serve the engine)
+    uint32_t life_lds = 0;
 };
 
 thread_local std::string g_create_err;    // brc_last_error(NULL): the last brc_create failure
@@ -224,18 +231,41 @@ static void free_all(Engine* e) {
     if (e->stream) (void)hipStreamDestroy(e->stream);
 }
 
-static int clear_state(Engine* e, bool full) {
+static int fill_cells(Engine* e) {
     const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
+    const uint64_t fb = std::min<uint64_t>((cells + 255) / 256, 1u << 20);
+    if (e->compact)
+        hipLaunchKernelGGL(fill_words<uint32_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, (uint32_t*)e->cells,
+                           C32_FRESH, (uint64_t)cells);
+    else
+        hipLaunchKernelGGL(fill_words<uint64_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, e->cells, TIMES_NEVER,
+                           (uint64_t)cells);
+    HIPCHK(e, hipGetLastError());
+    return BRC_OK;
+}
+
+// the step kernel's cells, allocated at its first launch on an engine the lifetime kernel may serve
+static int ensure_cells(Engine* e) {
+    if (e->cells_ready) return BRC_OK;
+    const size_t bytes = (size_t)e->nitems * e->rows * e->lpi * (e->compact ? 4 : 8);
+    if (e->cells) (void)hipFree(e->cells);
+    e->cells = nullptr;
+    if (hipMalloc(&e->cells, std::max<size_t>(bytes, 8)) != hipSuccess) {
+        (void)hipGetLastError();
+        e->err = "device allocation of " + std::to_string(bytes) + " B of step-kernel cells failed";
+        return BRC_E_NOMEM;
+    }
+    e->cells_ready = true;
+    return fill_cells(e);
+}
+
+static int clear_state(Engine* e, bool full) {
     const size_t keys = (size_t)e->cfg.instances * e->NK;
     if (full) {
-        const uint64_t fb = std::min<uint64_t>((cells + 255) / 256, 1u << 20);
-        if (e->compact)
-            hipLaunchKernelGGL(fill_words<uint32_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, (uint32_t*)e->cells,
-                               C32_FRESH, (uint64_t)cells);
-        else
-            hipLaunchKernelGGL(fill_words<uint64_t>, dim3((uint32_t)fb), dim3(256), 0, e->stream, e->cells, TIMES_NEVER,
-                               (uint64_t)cells);
-        HIPCHK(e, hipGetLastError());
+        if (e->cells_ready) {
+            const int rc = fill_cells(e);
+            if (rc) return rc;
+        }
         HIPCHK(e, hipMemsetAsync(e->meta, 0, keys * 8, e->stream));
         HIPCHK(e, hipMemsetAsync(e->mgen, 0, keys * 4, e->stream));
         e->gen_base = 0;
@@ -379,6 +409,20 @@ int brc_create(const brc_config* cfg, void** out) {
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
                                                 c.variants, e->rs, e->compact) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
+    // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8,
+    // proposals from Philox or loaded, no event log, no Byzantine pattern.  BRC_KERNEL=step | life |
+    // auto (default): auto runs connection-identity peers on it (their step-kernel cells are 5 words);
+    // sender peers stay on the step kernel, which is faster there
+    {
+        const char* kv = getenv("BRC_KERNEL");
+        const bool force_step = kv && strcmp(kv, "step") == 0, force_life = kv && strcmp(kv, "life") == 0;
+        e->life_lds = lds_bytes_life(e->NK, e->nkw, spec, c.key_window, c.variants);
+        const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
+                              c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
+                              (c.delay_model == BRC_DELAY_CONST || c.delay_model == BRC_DELAY_SLOWSET) &&
+                              c.delay_max <= 8 && e->life_lds <= 64 * 1024;
+        e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION);
+    }
     if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
         delete e;
@@ -395,7 +439,7 @@ int brc_create(const brc_config* cfg, void** out) {
     const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
     const size_t keys = (size_t)c.instances * e->NK;
     struct A { void** p; size_t bytes; } allocs[] = {
-        {(void**)&e->cells, cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
+        {(void**)&e->cells, e->life_cfg ? 8 : cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
         {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
@@ -414,6 +458,7 @@ int brc_create(const brc_config* cfg, void** out) {
         if (hipMalloc(&e->events, (size_t)c.event_capacity * sizeof(brc_event)) != hipSuccess) return fail(BRC_E_NOMEM);
         if (hipMalloc(&e->event_count, 8) != hipSuccess) return fail(BRC_E_NOMEM);
     }
+    e->cells_ready = !e->life_cfg;
     if (hipMemsetAsync(e->inj_off, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);
@@ -522,6 +567,10 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         }
         const uint64_t item = x.instance / e->ipw;
         if (its[item].initialized != 0 && x.t < its[item].t) { e->err = "injection time is before the instance's current step"; return BRC_E_STATE; }
+        if (ist[x.instance].status == BRC_QUIESCENT && e->life_done) {
+            e->err = "instance finished by the key-lifetime kernel (no step state to resume): brc_reset first";
+            return BRC_E_STATE;
+        }
         if (ist[x.instance].status == BRC_QUIESCENT) reopen.push_back(x.instance);
         else if (ist[x.instance].status != BRC_RUNNING) { e->err = "instance already stopped"; return BRC_E_STATE; }
         staged.push_back(r);
@@ -550,13 +599,22 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     // slot generations are 13-bit (wide kernel 11-bit) tags: past the budget a stale cell could
     // read as current.  brc_reset clears fully once the budget is spent; a run that keeps stepping
     // one simulation without resetting must stop here instead of risking the wrap.
+    // The lean (compact-cell) kernels and the lifetime kernel keep no generation tags: a slot's row is
+    // rewritten at allocation, so only the 14-bit phase-index snapshot bounds them.
     const uint64_t gen_hard = (e->wide ? GEN_MASK_W : GEN_MASK) - 2;
-    if (e->gen_base + 2 >= gen_hard) {
+    if (!e->compact && e->gen_base + 2 >= gen_hard) {
         e->err = "slot generation budget exhausted: call brc_reset";
         return BRC_E_STATE;
     }
     int rc = upload_injections(e);
     if (rc) return rc;
+    bool no_inj = true;
+    for (const auto& v : e->pending) if (!v.empty()) { no_inj = false; break; }
+    const bool life = e->life_cfg && e->fresh && no_inj && max_steps == 0;
+    if (!life) {
+        rc = ensure_cells(e);
+        if (rc) return rc;
+    }
     Params P;
     memset(&P, 0, sizeof(P));
     P.n = c.n; P.f = c.f; P.D = c.delay_max; P.Q = c.key_window; P.NV = c.variants; P.NK = e->NK; P.nkw = e->nkw;
@@ -575,7 +633,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.mode = c.mode; P.coin_seed = c.coin_seed;
     // a slot allocated for phase index s has been reallocated at most gen_base + s/Q + 1 times
     // (and phase indices stay below 2^14 - 1: the narrow kernel's consensus snapshot keeps s + 1 in 14 bits)
-    P.s_limit = (uint32_t)std::min<uint64_t>(0x3FFEull, (gen_hard - 1 - e->gen_base) * c.key_window);
+    P.s_limit = e->compact ? 0x3FFEu : (uint32_t)std::min<uint64_t>(0x3FFEull, (gen_hard - 1 - e->gen_base) * c.key_window);
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
@@ -587,9 +645,16 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
     const int kmode = c.peer_mode == BRC_PEER_CONNECTION ? KMODE_CONN : (int)c.mode;
-    rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)
-                    : launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
-                                  e->dparams);
+    e->fresh = false;
+    e->last_life = life;
+    if (life) {
+        rc = launch_life(kmode, (uint32_t)e->nitems, e->life_lds, e->stream, e->dparams);
+        e->life_done = true;
+    } else {
+        rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)
+                        : launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
+                                      e->dparams);
+    }
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }
     HIPCHK(e, hipEventRecord(e->ev1, e->stream));
@@ -597,7 +662,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
     unsigned long long gc[8];
     HIPCHK(e, hipMemcpy(gc, e->gcount, sizeof(gc), hipMemcpyDeviceToHost));
-    e->gen_cur = std::max<uint64_t>(e->gen_cur, gc[5] / c.key_window + 2);   // gc[5]: max phase index this epoch
+    if (!e->compact) e->gen_cur = std::max<uint64_t>(e->gen_cur, gc[5] / c.key_window + 2);   // gc[5]: max phase index
     if (running_left) *running_left = (uint32_t)gc[6];   // counted by the step kernel
     return BRC_OK;
 }
@@ -621,6 +686,8 @@ int brc_reset(void* h) {
         HIPCHK(e, hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream));
     }
     e->inj_dirty = false;
+    e->fresh = true;
+    e->life_done = false;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BRC_OK;
 }
@@ -803,6 +870,13 @@ int brc_read_events_range(void* h, size_t first, brc_event* out, size_t cap, siz
     if (out && cap && first < avail)
         HIPCHK(e, hipMemcpy(out, e->events + first, std::min(avail - first, cap) * sizeof(brc_event),
                             hipMemcpyDeviceToHost));
+    return BRC_OK;
+}
+
+int brc_last_kernel(void* h, uint32_t* kind) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || !kind) return BRC_E_INVALID;
+    *kind = e->last_life ? BRC_KERNEL_LIFE : BRC_KERNEL_STEP;
     return BRC_OK;
 }
 

@@ -163,6 +163,18 @@ inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32
     return spec ? (uint64_t)Q * lanes * ((wide || nv == 1 ? 0 : msize) + 4) : 4ull * lanes * msize;
 }
 
+// Key-lifetime kernel (brc_life.h): ring steps (> 4 Dd - 1 for Dd <= 8) and LDS bytes of one wave
+// (must match the kernel's carve):
+//   meta[NK] u32 | snap[NK] u16 (padded to 8 B) | dkA[RW][nkw] u64 | dkB[RW][nkw] u64 |
+//   ring[RW] {u64 arrivals | msgs, u64 cells | deliveries} | consensus area (cons_words at NPAD = 64) |
+//   pr[64] u32 (connection peers: READY copies per relative step and receiver class)
+constexpr uint32_t LIFE_RW = 32;
+__host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, uint32_t nkw, bool spec, uint32_t Q, uint32_t nv) {
+    return 4 * NK + ((2 * NK + 7) & ~7u) + 2 * LIFE_RW * nkw * 8 + LIFE_RW * 16 + 8 * cons_words(spec, 8, Q, nv) + 256;
+}
+// Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
+int launch_life(int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.
 int launch_step_4(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);

@@ -1,0 +1,568 @@
+// brc_life.h -- the key-lifetime kernel: batched Bracha broadcast + randomized consensus for
+// n <= 64 replicas (NPAD = 64, one instance per wavefront) under a two-class link-delay model.
+//
+// Why a second kernel.  The step kernel (brc_step.h) advances every live key one simulated step
+// at a time: per (key, step) it loads the key's 64 receiver cells from HBM, applies the handler
+// and stores them back, so a key costs one HBM round trip, a key-list entry and a metadata read
+// per active step.  But the BRB state of one key never depends on any other key
+// (core/brbroadcast.py:60-119 touches echo_sent_list[m], ready_sent_list[m] and the delivered
+// flag of m only), and a key is created by a SEND whose whole future is fixed at that moment.  So
+// this kernel simulates a key's ENTIRE lifetime -- every step at which one of its messages lands
+// -- right when the key is created, with the 64 receiver cells in registers; nothing of the key
+// goes to HBM.  What leaves the lifetime simulation is (a) for each future step, the keys some
+// receivers deliver then (consumed by the consensus pass of that step, in canonical key order,
+// exactly as the step kernel does) and (b) per-step statistics.  Both live in LDS rings indexed
+// by step mod RW; the consensus step loop commits a step's statistics when it reaches it, so an
+// instance that stops at step T counts exactly the events of steps <= T.
+//
+// Two-class delays.  Under the constant and slow-set models a link's delay
+// is 1 when both ends are "fast" and Dd otherwise (constant: no fast class, Dd = the constant).
+// Every receiver of a class therefore sees the same arrival counts; they are computed once per
+// class with scalar popcounts of the senders' ballots (two per message type) and selected per
+// lane.  The per-receiver cell update still runs on every lane.  Receivers of one class evolve
+// identically, so a key's deliveries at a step are whole honest classes; the consensus pass
+// reads them as two per-class key bitmaps per step.  A key's messages all land within 4 Dd steps
+// of its SEND (ECHO <= Dd, READY <= 3 Dd: a class READYs by quorum or is amplified by the other),
+// so RW = 32 covers Dd <= 8; the host uses this kernel only there (brc_engine.hip).
+//
+// Connection-identity peers (core/brbroadcast.py:69, KMODE_CONN): sets count messages and the :119
+// amplification re-fires, so a lane may send several READY copies at several steps; the copies
+// landing at each relative step are summed per receiver class at send time into a per-key LDS ring
+// (s_pr) instead of ballots over one send step per lane.
+//
+// Scope (host-checked): sender- or connection-identity peers, consensus protocol with Philox or loaded
+// proposals, constant or slow-set delays with D <= 8, no injections, no event log, a fresh
+// engine run to completion.  Everything else runs on the step kernel.  Results are identical to
+// the step kernel's (tests/test_gpu_life.py checks both against the C oracle).
+#pragma once
+#include "brc_step.h"
+
+namespace brc {
+
+constexpr uint32_t LIFE_NEVER = 0xFFFFu;         // relative send step: not sent
+
+// meta word of a key slot: low 16 bits = value << 14 | (s + 1) (the consensus snapshot format),
+// high 16 bits = the last step with an arrival of the key at an honest receiver (slot busy before it)
+__device__ __forceinline__ uint32_t lm_s1(uint32_t m) { return m & 0x3FFFu; }
+__device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
+
+template <int MODE>
+__global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp) {
+    const Params& P = *pp;
+    constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
+    constexpr uint32_t RW = LIFE_RW;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t item = blockIdx.x;
+    if (item >= P.nitems) return;
+    const uint32_t n = P.n, NK = P.NK, Q = P.Q, NV = P.NV, nkw = P.nkw;
+    const uint32_t T_echo = P.T_echo, T_amp = P.T_amp, T_del = P.T_del;
+    const uint32_t qsh = (uint32_t)__ffs(Q) - 1u, Qm = Q - 1u, ksh = qsh + (uint32_t)__ffs(NV) - 1u;
+    const bool seen_on = NV > 1;
+
+    // ---- LDS carve (lds_bytes_life)
+    uint32_t* s_meta = (uint32_t*)smem;
+    uint16_t* s_snap = (uint16_t*)(s_meta + NK);
+    uint64_t* s_dkA = (uint64_t*)((char*)smem + 4 * NK + ((2 * NK + 7) & ~7u));
+    uint64_t* s_dkB = s_dkA + RW * nkw;
+    uint64_t* s_ring = s_dkB + RW * nkw;          // [row][2]: arrivals | msgs << 32, cells | deliveries << 32
+    uint64_t* s_hm = s_ring + 2 * RW;             // REFERENCE / BEB: hosts per value [4][64]
+    uint64_t* s_seen = s_hm;                      // SPEC, NV > 1: [Q][64]
+    uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));   // SPEC: [Q][64]
+    // CONN: READY copies landing at relative step r of the key being simulated, per receiver class:
+    // fast | slow << 16 (a lane may send several READY copies, at several steps: counts, not ballots)
+    uint32_t* s_pr = (uint32_t*)(s_hm + cons_words(SPEC, 8, Q, NV));
+
+    const uint32_t d = lane;
+    const uint64_t inst = item;                   // one instance per wave
+    const uint64_t g = P.inst_offset + inst;
+    const uint64_t byzm = gp(P.byz)[inst];
+    const bool real = d < n;
+    const bool honest = real && !((byzm >> d) & 1ull);
+    const uint64_t real_mask = (n >= 64) ? ~0ull : ((1ull << n) - 1);
+    const uint64_t hon_mask = uni64(__ballot(honest));
+    auto lane_in = [](uint64_t mask) -> bool { return __builtin_amdgcn_inverse_ballot_w64(mask); };
+    auto wave_sum = [](uint32_t x) -> uint32_t {
+#pragma unroll
+        for (int o = 32; o; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+        return uni32(x);
+    };
+
+    // ---- two delay classes: delay(j -> d) = 1 if j and d are both fast, Dd otherwise
+    uint64_t Fm = 0;                               // real fast replicas
+    uint32_t Dd = P.delay_model == BRC_DELAY_CONST ? P.dconst : P.D;
+    if (P.delay_model == BRC_DELAY_SLOWSET && P.D > 1) {
+        const uint32_t off = slow_offset(P.seed, g, n);
+        const bool slow = ((d + n - off) % n) < P.f;
+        Fm = uni64(__ballot(real && !slow));
+    } else if (P.delay_model == BRC_DELAY_SLOWSET) {
+        Dd = 1;                                    // D = 1: every link has delay 1
+    }
+    Dd = uni32(Dd);
+    const uint64_t Sm = real_mask & ~Fm;
+    const uint64_t HF = Fm & hon_mask, HS = Sm & hon_mask;
+    const uint32_t nHF = (uint32_t)__popcll(HF), nHS = (uint32_t)__popcll(HS);
+    const bool laneF = lane_in(Fm);
+
+    // ---- LDS init
+    for (uint32_t i = lane; i < NK; i += 64) { s_meta[i] = 0; s_snap[i] = 0; }
+    for (uint32_t i = lane; i < 2 * RW * nkw; i += 64) s_dkA[i] = 0;
+    for (uint32_t i = lane; i < 2 * RW; i += 64) s_ring[i] = 0;
+    if constexpr (SPEC) {
+        for (uint32_t q = 0; q < Q; ++q) {
+            if (seen_on) s_seen[q * 64 + lane] = 0;
+            s_cnt[q * 64 + lane] = 0;
+        }
+    } else {
+        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+    uint32_t status = BRC_RUNNING, t_stop = 0, t = 0;
+    bool ovf = false;
+    // committed statistics (wave-uniform) and per-lane work counters
+    uint64_t tot_arr = 0, tot_msg = 0, tot_cell = 0, tot_del = 0, key_steps = 0;
+    uint32_t st_smax = 0;
+    uint32_t rows = 0;                             // ring rows holding arrivals at honest receivers
+
+    // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
+    const bool cons_lane = honest;                 // consensus protocol (host-checked)
+    uint32_t round = 0, phase = 0, nvals = 0, order = 0, vcount = 0;
+    uint32_t dcount = 0, frnd = 0, ft = 0, fval = 0, lval = 0;
+    uint32_t clr = 0;                              // this lane's key slots created this step (bit s mod Q)
+    uint32_t msg_now = 0;                          // SEND messages sent this step (per lane, counted at once)
+
+    // honest origin d broadcasts SEND for its key (d, s) with value v (core/byzantinerandomizedconsensus.py:48-50,
+    // :80-83, :102-106): the slot is claimed now, its lifetime is simulated after the step (simulate below)
+    auto send_key = [&](uint32_t s, uint32_t v) {
+        const uint32_t k = (d * NV) * Q + (s & Qm);
+        const uint32_t m = s_meta[k];
+        if ((lm_s1(m) != 0 && t < lm_tend(m)) || s >= 0x3FFEu) { ovf = true; return; }
+        s_meta[k] = ((t + 1u) << 16) | ((v & 3u) << 14) | (s + 1u);   // busy until simulated
+        clr |= 1u << (s & Qm);
+        msg_now += n;
+        st_smax = max(st_smax, s);
+    };
+    auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
+        for (uint32_t i = 0; i < nvals; ++i) {
+            const uint32_t v = (order >> (2 * i)) & 3;
+            if (2 * (uint32_t)__popcll(s_hm[v * 64 + lane]) > bound2) return v;
+        }
+        return 0;                                                    // str(NONE) == "-1"
+    };
+    auto cons_reset = [&]() {
+        vcount = 0; nvals = 0; order = 0;
+        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
+    };
+    auto cons_deliver_vh = [&](uint32_t v, uint32_t host) {          // :53-106
+        const uint32_t x = order ^ (v * 0x55u);
+        const uint32_t valid = (1u << (2 * nvals)) - 1u;
+        const bool found = (~(x | (x >> 1)) & 0x55u & valid) != 0;
+        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
+        s_hm[v * 64 + lane] |= 1ull << host;                        // :60
+        ++vcount;                                                    // :61
+        if (vcount >= P.T_cnt && phase == 1) {                       // :71
+            const uint32_t prop = get_max_val(P.bound_p1);           // :73
+            phase = 2; cons_reset();                                 // :75-78
+            send_key(2 * (round - 1) + 1, prop);                     // :80-83
+        }
+        if (vcount >= P.T_cnt && phase == 2) {                       // :86
+            const uint32_t dec = get_max_val(P.bound_p2);            // :88 (:89 is always False: decide runs)
+            ++dcount;
+            if (dcount == 1) { frnd = round; ft = t; fval = dec; }
+            lval = dec;
+            ++round; phase = 1; cons_reset();                        // :96-100
+            send_key(2 * (round - 1), dec);                          // :102-106
+        }
+    };
+    // SPEC consensus (oracle spec_advance / spec_deliver; brc_step.h)
+    auto spec_advance = [&]() {
+        while (round > 0) {
+            const uint32_t s = 2 * (round - 1) + (phase - 1), q = s & Qm;
+            const uint32_t cc = s_cnt[q * 64 + lane], n0 = (cc >> 10) & 0x3FF, n1 = cc >> 20;
+            if ((seen_on ? (uint32_t)__popcll(s_seen[q * 64 + lane]) : (cc & 0x3FF)) < n - P.f) return;
+            if (seen_on) s_seen[q * 64 + lane] = 0;
+            s_cnt[q * 64 + lane] = 0;
+            if (phase == 1) {
+                const uint32_t prop = (2 * n0 > n + P.f) ? 1u : (2 * n1 > n + P.f) ? 2u : 0u;
+                phase = 2;
+                send_key(s + 1, prop);
+            } else {
+                const uint32_t vmax = n1 > n0 ? 2u : 1u, cmax = max(n0, n1);
+                uint32_t est;
+                if (cmax > 2 * P.f) {
+                    ++dcount;
+                    if (dcount == 1) { frnd = round; ft = t; fval = vmax; }
+                    lval = vmax;
+                    est = vmax;
+                } else if (cmax > P.f) {
+                    est = vmax;
+                } else {
+                    est = coin_id(P.coin_seed, g, round);
+                }
+                ++round; phase = 1;
+                send_key(s + 1, est);
+            }
+        }
+    };
+    auto spec_deliver = [&](uint32_t k) {
+        const uint32_t sn = s_snap[k];
+        const uint32_t s = (sn & 0x3FFFu) - 1u, v = sn >> 14, host = k >> ksh;
+        const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
+        if (s < cur) return;
+        if (s >= cur + Q) { ovf = true; return; }
+        const uint32_t q = s & Qm;
+        if (seen_on) {
+            if ((s_seen[q * 64 + lane] >> host) & 1) return;
+            s_seen[q * 64 + lane] |= 1ull << host;
+        }
+        s_cnt[q * 64 + lane] += 1u + (v == 1 ? 1u << 10 : 0u) + (v == 2 ? 1u << 20 : 0u);
+        spec_advance();
+    };
+
+    // ---- the lifetime of key slot k created at step t (wave-uniform): every step at which one of
+    // its messages lands on an honest receiver, in order; cells in registers (brc_step.h C32 fields
+    // unpacked: flags, |echo set|, |ready set|, and the relative steps this lane SENT ECHO / READY)
+    auto simulate = [&](uint32_t k) {
+        const uint32_t o = k >> ksh;                  // origin
+        const bool oF = (Fm >> o) & 1ull;
+        const uint32_t t0 = t;
+        // SEND arrivals: fast receivers at 1 if the origin is fast, everyone else at Dd
+        const uint32_t sdl = (oF && laneF) ? 1u : Dd;
+        uint64_t pendS = 0, pendE = 0, pendR = 0;     // relative steps with SEND / ECHO / READY arrivals
+        if (oF && HF) pendS |= 1ull << 1;
+        if (HS || (!oF && HF)) pendS |= 1ull << Dd;
+        uint32_t fl = 0, ec = 0, rc = 0, rE = LIFE_NEVER, rR = LIFE_NEVER;
+        uint32_t last = t0;
+        if constexpr (CONN) s_pr[lane] = 0;
+        const uint32_t kw = k >> 6;
+        const uint64_t kbit = 1ull << (k & 63);
+        for (uint64_t pend = pendS; pend; pend = pendS | pendE | pendR) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(pend);
+            const uint64_t rb = 1ull << r;
+            const bool hS = (pendS & rb) != 0, hE = (pendE & rb) != 0, hR = (pendR & rb) != 0;
+            pendS &= ~rb; pendE &= ~rb; pendR &= ~rb;
+            if (r > RW) { ovf = true; break; }        // cannot happen for Dd <= 8 (lifetime <= 4 Dd)
+            const uint32_t ts = t0 + r, row = ts & (RW - 1);
+            ++key_steps;
+            // arrival counts per receiver class (fast: fast senders at r - 1, slow senders at r - Dd;
+            // slow: every sender at r - Dd), then per lane
+            const uint32_t c1 = r - 1u, cD = r >= Dd ? r - Dd : 0xFFFFFFFFu;
+            uint32_t ea = 0, ra = 0, eA = 0, eB = 0, rA = 0, rB = 0;
+            if (hE) {
+                const uint64_t x1 = __ballot(rE == c1), xD = __ballot(rE == cD);
+                eA = (uint32_t)__popcll(x1 & Fm) + (uint32_t)__popcll(xD & Sm);
+                eB = (uint32_t)__popcll(xD);
+                ea = laneF ? eA : eB;
+            }
+            if (hR) {
+                if constexpr (CONN) {
+                    const uint32_t ab = uni32(s_pr[r]);
+                    rA = ab & 0xFFFFu; rB = ab >> 16;
+                } else {
+                    const uint64_t x1 = __ballot(rR == c1), xD = __ballot(rR == cD);
+                    rA = (uint32_t)__popcll(x1 & Fm) + (uint32_t)__popcll(xD & Sm);
+                    rB = (uint32_t)__popcll(xD);
+                }
+                ra = laneF ? rA : rB;
+            }
+            const uint32_t sa = (hS && honest && r == sdl) ? 1u : 0u;
+            const uint64_t sab = hS ? __ballot(sa != 0) : 0ull;
+            const uint32_t a = ea + ra + sa;
+            const uint64_t hb = __ballot(a != 0) & hon_mask;          // receivers with arrivals
+            const uint32_t cells = (uint32_t)__popcll(hb);
+            const uint32_t arr = nHF * (eA + rA) + nHS * (eB + rB) + (uint32_t)__popcll(sab);
+            // a delivered cell ignores everything (core/brbroadcast.py:74)
+            const bool opn = lane_in(hb) && !(fl & F_DEL);
+            auto ge = [](uint32_t x, uint32_t y) -> uint32_t { return ((x - y) >> 31) ^ 1u; };   // x >= y (< 2^31)
+            uint32_t es = 0, rs = 0, dl = 0, nr = 0;
+            if constexpr (CONN) {
+                // core/brbroadcast.py:60-119 with connection-identity peers (brc_step.h brb_cell_update_conn):
+                // sets count messages; the :119 amplification re-fires, nr READY copies this step
+                bool esb, dlb;
+                brb_cell_update_conn(fl, ec, rc, opn && sa, opn ? ea : 0u, opn ? ra : 0u, T_echo, T_amp, T_del, esb, nr,
+                                     dlb);
+                fl |= nr ? F_RS : 0u;
+                es = esb ? 1u : 0u; rs = nr ? 1u : 0u; dl = dlb ? 1u : 0u;
+            } else if constexpr (BEB) {
+                dl = (opn && sa) ? 1u : 0u;                             // brb_cell_update_beb
+                fl |= dl << 2;
+            } else if constexpr (SPEC) {
+                if (hS) { es = (opn ? sa : 0u) & ~(fl >> 3) & 1u; fl |= es << 3; }   // brb_cell_update_spec
+                if (hE || hR) {
+                    ec += opn ? ea : 0u;
+                    rc += opn ? ra : 0u;
+                    rs = (opn ? 1u : 0u) & ~(fl >> 4) & (ge(ec, T_echo) | ge(rc, T_amp));
+                    fl |= rs << 4;
+                    dl = (opn ? 1u : 0u) & ge(rc, T_del);
+                    fl |= dl << 2;
+                }
+            } else {
+                // brb_cell_update in integer form (brc_step.h process_pair).  F_EEX = bit 0, F_REX = 1,
+                // F_DEL = 2, F_ES = 3, F_RS = 4.
+                if (hS) {                                                // :76-82
+                    es = (opn ? sa : 0u) & ~fl & 1u;
+                    fl |= es | (es << 3);
+                }
+                if (hE) {                                                // :84-98
+                    const uint32_t e = opn ? ea : 0u;
+                    const uint32_t eon = min(e, 1u);
+                    const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
+                    fl |= eon;
+                    ec += e;
+                    const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
+                    fl |= (r1 << 1) | (r1 << 4);
+                    rs = r1;
+                }
+                if (hR) {                                                // :100-119
+                    const uint32_t x = opn ? ra : 0u;
+                    const uint32_t ron = min(x, 1u);
+                    const uint32_t rexm = 0u - ((fl >> 1) & 1u);
+                    const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
+                    fl |= ron << 1;
+                    rc += x;
+                    const uint32_t any = ron & ge(rhi, rlo);
+                    const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+                    const uint32_t r2 = any & ~fl & ~(fl >> 4) & ge(ahi, alo) & 1u;
+                    fl |= r2 << 4;
+                    dl = any & ge(rhi, T_del);
+                    fl |= dl << 2;
+                    rs |= r2;
+                }
+            }
+            const uint64_t eb = __ballot(es != 0), rbm = __ballot(rs != 0), db = __ballot(dl != 0);
+            if (es) rE = r;
+            if (!CONN && rs) rR = r;
+            // READY messages sent now by fast / slow senders (CONN: copies, a lane may send several)
+            uint32_t cF = (uint32_t)__popcll(rbm & Fm), cS = (uint32_t)__popcll(rbm & Sm);
+            if constexpr (CONN) {
+                if (__ballot(nr > 1)) {                                  // bit planes of the per-lane counts
+                    cF = cS = 0;
+                    for (uint32_t b = 0; b < 8; ++b) {
+                        const uint64_t pb = __ballot((nr >> b) & 1u);
+                        cF += (uint32_t)__popcll(pb & Fm) << b;
+                        cS += (uint32_t)__popcll(pb & Sm) << b;
+                    }
+                }
+            }
+            const uint32_t msgs = n * ((uint32_t)__popcll(eb) + cF + cS);
+            const uint32_t dels = (uint32_t)__popcll(db);
+            if (db) {
+                // receivers of one class evolve identically: a delivery step takes whole honest classes
+                const uint64_t dA = db & HF, dB = db & HS;
+                if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
+                if (dA && lane == 0) s_dkA[row * nkw + kw] |= kbit;
+                if (dB && lane == 0) s_dkB[row * nkw + kw] |= kbit;
+            }
+            // the messages sent now land on fast receivers after 1 step (fast senders) and on every
+            // other (sender, receiver) pair after Dd steps
+            if (eb) {
+                if ((eb & Fm) && HF) pendE |= rb << 1;
+                if (HS || ((eb & Sm) && HF)) pendE |= rb << Dd;
+            }
+            if (rbm) {
+                const bool at1 = cF && HF, atD = HS || (cS && HF);
+                if (at1) pendR |= rb << 1;
+                if (atD) pendR |= rb << Dd;
+                if constexpr (CONN) {
+                    if (lane == 0) {
+                        if (at1) s_pr[r + 1] += cF;
+                        if (atD) s_pr[r + Dd] += cS + ((cF + cS) << 16);
+                    }
+                }
+            }
+            if (lane == 0) {
+                s_ring[2 * row] += (uint64_t)arr | ((uint64_t)msgs << 32);
+                s_ring[2 * row + 1] += (uint64_t)cells | ((uint64_t)dels << 32);
+            }
+            rows |= 1u << row;
+            last = ts;
+        }
+        if (lane == 0) s_meta[k] = (s_meta[k] & 0xFFFFu) | (last << 16);
+    };
+    // the keys created this step (clr bits of every lane), each simulated once
+    auto simulate_new = [&]() {
+        for (uint64_t b = __ballot(clr != 0); b; b &= b - 1) {
+            const int L = __ffsll((unsigned long long)b) - 1;
+            for (uint32_t cm = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr, L)); cm; cm &= cm - 1) {
+                const uint32_t k = ((uint32_t)L * NV) * Q + (uint32_t)__ffs(cm) - 1u;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                simulate(k);
+            }
+        }
+        clr = 0;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    };
+
+    // ---- step 0: the proposals (actions stamped 0, core/byzantinerandomizedconsensus.py:38-50)
+    if (honest) {
+        const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? proposal_id(P.seed, g, d)
+                                                                 : (uint32_t)gp(P.prop)[inst * n + d];
+        round = 1; phase = 1;
+        send_key(0, v & 3);
+        if constexpr (SPEC) spec_advance();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    tot_msg += wave_sum(msg_now);
+    msg_now = 0;
+    if (__ballot(ovf)) status = BRC_OVERFLOW;
+    else simulate_new();
+
+    const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
+    while (status == BRC_RUNNING) {
+        // next step with arrivals at an honest receiver
+        const uint32_t rot = (t + 1) & (RW - 1);
+        const uint32_t rr = rot ? ((rows >> rot) | (rows << (RW - rot))) : rows;
+        if (!rr) { status = BRC_QUIESCENT; break; }
+        const uint32_t next = t + 1 + (uint32_t)__ffs(rr) - 1u;
+        if (next > P.step_cap) { status = BRC_STEPCAP; break; }
+        t = uni32(next);
+        const uint32_t row = t & (RW - 1);
+        // commit the step's statistics
+        {
+            const uint64_t a = s_ring[2 * row], c = s_ring[2 * row + 1];
+            tot_arr += (uint32_t)a; tot_msg += a >> 32; tot_cell += (uint32_t)c; tot_del += c >> 32;
+            if ((uint32_t)c) t_stop = t;
+        }
+        // ================= consensus: this step's deliveries in canonical (kp, s) order
+        for (uint32_t i = lane; i < NK; i += 64) s_snap[i] = (uint16_t)s_meta[i];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll 1
+        for (uint32_t w = 0; w < nkw; ++w) {
+            const uint64_t kA = s_dkA[row * nkw + w], kB = s_dkB[row * nkw + w];
+            uint64_t bits = cons_lane ? (laneF ? kA : kB) : 0ull;
+            if constexpr (SPEC) {
+                // word at once when every delivering lane is at one phase index c0 and its current-phase
+                // deliveries cannot complete the phase (brc_step.h, SPEC consensus pass)
+                const uint64_t hb = __ballot(bits != 0);
+                if (!seen_on && hb) {
+                    const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
+                    const uint32_t c0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)hb) - 1));
+                    if (!__ballot(bits != 0 && cur != c0)) {
+                        const uint32_t sn = s_snap[w * 64 + lane];
+                        const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;
+                        const uint64_t inw = __ballot(ss >= c0 && ss - c0 < Q), atc = __ballot(ss == c0);
+                        const uint64_t past = __ballot(ss != 0xFFFFFFFFu && ss >= c0 && ss - c0 >= Q);
+                        const uint64_t v1 = __ballot(sv == 1), v2 = __ballot(sv == 2);
+                        const uint32_t ncur = (uint32_t)__popcll(bits & atc);
+                        const uint32_t qc = c0 & Qm;
+                        if (bits && (round == 0 || (s_cnt[qc * 64 + lane] & 0x3FFu) + ncur < n - P.f)) {
+                            if (bits & past) ovf = true;
+                            const uint64_t b = bits & inw;
+                            const uint64_t g0 = Q == 2 ? 0x5555555555555555ull : Q == 4 ? 0x1111111111111111ull
+                                                                                : 0x0101010101010101ull;
+                            for (uint32_t q = 0; q < Q; ++q) {
+                                const uint64_t bq = b & (g0 << q);
+                                if (bq) s_cnt[q * 64 + lane] += (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
+                                                                 ((uint32_t)__popcll(bq & v2) << 20);
+                            }
+                            bits = 0;
+                        }
+                    }
+                }
+            } else {
+                // word at once when no phase can change (brc_step.h, REFERENCE consensus pass)
+                if (__ballot(bits != 0)) {
+                    const uint32_t sv = (uint32_t)s_snap[w * 64 + lane] >> 14;
+                    const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
+                    const uint32_t nb = (uint32_t)__popcll(bits);
+                    const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
+                    if (nb && oneper && ((phase != 1 && phase != 2) || vcount + nb < P.T_cnt)) {
+                        const uint32_t G = Q * NV, opw = 64u / G;
+                        uint32_t first[4];
+#pragma unroll
+                        for (int v = 0; v < 4; ++v) {
+                            const uint64_t dv = bits & vm[v];
+                            first[v] = dv ? (uint32_t)__ffsll((unsigned long long)dv) - 1u : 64u;
+                            if (dv) s_hm[v * 64 + lane] |= compress_groups(fold_groups(dv, G), G) << (w * opw);
+                            const uint32_t xo = order ^ ((uint32_t)v * 0x55u);
+                            if (((~(xo | (xo >> 1)) & 0x55u & ((1u << (2 * nvals)) - 1u)) != 0)) first[v] = 64u;
+                        }
+                        for (int r = 0; r < 4; ++r) {
+                            uint32_t bv = 0, bp = 64u;
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) if (first[v] < bp) { bp = first[v]; bv = (uint32_t)v; }
+                            if (bp == 64u) break;
+                            order |= bv << (2 * nvals); ++nvals;
+#pragma unroll
+                            for (int v = 0; v < 4; ++v) if ((uint32_t)v == bv) first[v] = 64u;
+                        }
+                        vcount += nb;
+                        bits = 0;
+                    }
+                }
+            }
+            // one delivery at a time, ascending slot; several phases of one key prefix: smallest s first
+            while (bits) {
+                uint32_t best = __ffsll((unsigned long long)bits) - 1;
+                const uint64_t grp = bits & (gm0 << (best & ~Qm));
+                if (grp & (grp - 1)) {
+                    uint32_t bs = 0xFFFFFFFFu;
+                    for (uint64_t x = grp; x; x &= x - 1) {
+                        const uint32_t bb = __ffsll((unsigned long long)x) - 1;
+                        const uint32_t s1 = s_snap[w * 64 + bb] & 0x3FFFu;
+                        if (s1 < bs) { bs = s1; best = bb; }
+                    }
+                }
+                bits &= ~(1ull << best);
+                if constexpr (SPEC) spec_deliver(w * 64 + best);
+                else cons_deliver_vh((uint32_t)s_snap[w * 64 + best] >> 14, (w * 64 + best) >> ksh);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        tot_msg += wave_sum(msg_now);
+        msg_now = 0;
+        // the step is consumed: its ring row is free for step t + RW
+        if (lane < 2 * nkw) (lane < nkw ? s_dkA : s_dkB)[row * nkw + (lane % nkw)] = 0;
+        if (lane < 2) s_ring[2 * row + lane] = 0;
+        rows &= ~(1u << row);
+        // ================= per-instance stop conditions (brc_step.h)
+        const uint64_t b_und = __ballot(honest && dcount < P.round_cap);
+        if (__ballot(ovf)) status = BRC_OVERFLOW;
+        else if (P.round_cap > 0 && !b_und) status = BRC_DONE;
+        else simulate_new();                          // the keys this step's consensus created
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (__ballot(ovf) && status != BRC_OVERFLOW) status = BRC_OVERFLOW;
+
+    // ---- write back (result readers: inst, istats, items, cons0/cons1, gcount)
+    if (lane == 0) {
+        gptr_t<uint64_t> ip = (gptr_t<uint64_t>)&gp(P.inst)[inst];
+        *ip = (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) | ((uint64_t)(t & 0xFFFF) << 32);
+        gp(P.istats)[inst * 4 + 0] = tot_msg;
+        gp(P.istats)[inst * 4 + 1] = tot_arr;
+        gp(P.istats)[inst * 4 + 2] = tot_cell;
+        gp(P.istats)[inst * 4 + 3] = tot_del;
+        ItemState o = {t, 0u, 1u, 0u};
+        P.items[item] = o;
+        gp(P.actany)[item] = 0;
+    }
+    const size_t li = item * 64 + lane;
+    if (honest) {
+        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
+                          ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
+                          ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
+    }
+    uint32_t smax = st_smax;
+#pragma unroll
+    for (int o2 = 32; o2; o2 >>= 1) smax = max(smax, (uint32_t)__shfl_xor((int)smax, o2));
+    if (lane == 0) {
+        const unsigned long long w6[5] = {tot_cell, tot_arr, tot_msg, tot_del, key_steps * 64ull};
+#pragma unroll
+        for (int q = 0; q < 5; ++q) if (w6[q]) atomicAdd(&P.gcount[q], w6[q]);
+        if (smax) atomicMax(&P.gcount[5], (unsigned long long)smax);
+    }
+}
+
+template <int MODE>
+int launch_life_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    auto kern = brc_life<MODE>;
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return BRC_E_HIP;
+    kern<<<dim3(blocks), dim3(64), lds, s>>>(P);
+    return hipGetLastError() == hipSuccess ? 0 : BRC_E_HIP;
+}
+
+}  // namespace brc

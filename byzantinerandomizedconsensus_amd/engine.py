@@ -122,6 +122,12 @@ class Engine:
         self._chk(self._lib.brc_last_kernel_ms(self._h, ctypes.byref(ms)))
         return ms.value
 
+    def last_kernel(self):
+        """"step" or "life": the kernel the last run() launched (include/brc.h brc_last_kernel)."""
+        k = ctypes.c_uint32(0)
+        self._chk(self._lib.brc_last_kernel(self._h, ctypes.byref(k)))
+        return "life" if k.value == L.KERNEL_LIFE else "step"
+
     # ------------------------------------------------------------------ outputs
     def instances_result(self, first=0, count=None):
         count = self.instances - first if count is None else count

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 4
+#define BRC_ABI_VERSION 5
 
 enum {
     BRC_OK = 0,
@@ -180,6 +180,16 @@ int brc_reset_at(void* engine, uint64_t instance_offset);
  * since the last reset, dropped ones included.  Lets a caller drain the log incrementally. */
 int brc_read_events_range(void* engine, size_t first, brc_event* out, size_t cap, size_t* total);
 int brc_last_kernel_ms(void* engine, float* ms);
+/* Which kernel the last brc_run launched.  BRC_KERNEL_LIFE (the key-lifetime kernel) runs a fresh
+ * engine (after brc_create / brc_reset) to completion in one launch when the configuration allows:
+ * n in 33..64, consensus with Philox or loaded proposals, constant or slow-set delays with
+ * delay_max <= 8, no event log, no byz_pattern, no injections, max_steps == 0.  By default it runs
+ * connection-identity peers (BRC_PEER_CONNECTION); the environment variable BRC_KERNEL (read by
+ * brc_create) = life uses it for sender peers too, = step never.  Its results equal the step
+ * kernel's; its instances end final, so a later injection that would re-open a QUIESCENT instance
+ * is BRC_E_STATE until brc_reset. */
+enum { BRC_KERNEL_STEP = 0, BRC_KERNEL_LIFE = 1 };
+int brc_last_kernel(void* engine, uint32_t* kind);
 int brc_device_count(int* count);
 const char* brc_last_error(void* engine);   /* engine NULL: why the last brc_create on this thread failed */
 void brc_destroy(void* engine);

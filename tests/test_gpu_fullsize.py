@@ -19,6 +19,8 @@ import pytest
 from oracle import oracle
 from tests.golden import specs as S
 
+VID = {v: i for i, v in enumerate(S.VALUES)}     # the oracle reports decided values as strings
+
 pytestmark = pytest.mark.gpu
 
 
@@ -60,7 +62,7 @@ def _check_sample(res, reps, kw, base, ids, make_spec):
         if i in reps:
             first = {}
             for t, node, rnd, val in sorted(exp["events"]["decide"]):
-                first.setdefault(node, (rnd, t, val))
+                first.setdefault(node, (rnd, t, VID[val]))
             for d, rep in enumerate(reps[i]):
                 if d in sp.get("byzantine", []):
                     continue
@@ -134,7 +136,7 @@ def test_cfg4_bench_batch_full_size(mode):
             assert sub[j][k] == exp[k], (g, k)
         first = {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
-            first.setdefault(node, (rnd, t, val))
+            first.setdefault(node, (rnd, t, VID[val]))
         got = [(r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) for r in reps[j]]
         assert got == [first[d] for d in range(64)], g
 
@@ -173,7 +175,7 @@ def test_cfg5_n256_full_size(model, dmax):
         for d, (rep, exp) in enumerate(zip(reps[g], c["first_decide"])):
             assert exp is not None, (g, d)
             got = (rep["first_decide_round"], rep["first_decide_t"], rep["first_decide_value"])
-            assert got == tuple(exp), (model, g, d)
+            assert got == (exp[0], exp[1], VID[exp[2]]), (model, g, d)
 
 
 @pytest.mark.parametrize("mode", ["reference", "spec"])
@@ -207,7 +209,7 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
             assert res[g][k] == exp[k], (g, k)
         first = {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
-            first.setdefault(node, (rnd, t, val))
+            first.setdefault(node, (rnd, t, VID[val]))
         got = [(r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) for r in reps[g]]
         assert got == [first[d] for d in range(64)], g
         for d in range(64):
@@ -226,16 +228,22 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
 @pytest.mark.parametrize("mode", ["reference", "spec"])
 def test_cfg4_long_consensus_many_rounds(mode):
     """Long-running consensus at scale (the reference re-proposes forever,
-    core/byzantinerandomizedconsensus.py:96-106): 2^17 cfg4 instances run to round_cap = 8
+    core/byzantinerandomizedconsensus.py:96-106): 2^17 n=64 f=21 instances run to round_cap = 8
     decisions per replica, so slots recycle and the compact cells' epoch moves across many rounds
-    under a full batch.  Sampled instances equal the oracle (counters and every replica's first
-    and last decision, values included)."""
+    under a full batch.  SPEC runs the cfg4 slow-set schedule (D = 8); the reference protocol runs
+    constant delays D = 2, because its fast replicas cycle rounds faster than a phase window of 8
+    covers the D = 8 slow set (BRC_OVERFLOW).  Sampled instances equal the oracle
+    (counters and every replica's first and last decision, values included)."""
     L = _L()
     N, CAP = 1 << 17, 8
     spec = mode == "spec"
-    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
-              round_cap=CAP, step_cap=4000, key_window=8 if spec else 4, proposals=L.PROPOSALS_PHILOX,
-              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    if spec:
+        kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+                  round_cap=CAP, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC,
+                  coin_seed=0xC017C017)
+    else:
+        kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_CONST, delay_max=2,
+                  delay_const=2, round_cap=CAP, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX)
     ids = sorted(random.Random(8).sample(range(N), 6)) + [N - 1]
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
@@ -248,13 +256,13 @@ def test_cfg4_long_consensus_many_rounds(mode):
             exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8,
                                               coin_seed=0xC017C017))
         else:
-            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP))
+            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 0, 2, g, round_cap=CAP, dconst=2))
         for k in KEYS:
             assert res[g][k] == exp[k], (g, k)
         first, last, count = {}, {}, {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
-            first.setdefault(node, (rnd, t, val))
-            last[node] = val
+            first.setdefault(node, (rnd, t, VID[val]))
+            last[node] = VID[val]
             count[node] = count.get(node, 0) + 1
         for d, r in enumerate(reps[g]):
             assert (r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) == first[d], (g, d)

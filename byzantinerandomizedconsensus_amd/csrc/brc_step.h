@@ -160,14 +160,18 @@ __device__ __forceinline__ void brb_cell_update(uint32_t& fl, uint32_t& ec, uint
                                                 uint32_t ea, uint32_t ra, uint32_t T_echo, uint32_t T_amp,
                                                 uint32_t T_del, bool& echo_send, bool& ready_send, bool& deliver) {
     const bool open = !(fl & F_DEL);                                        // :74
-    echo_send = open && s_arr && !(fl & F_EEX);                             // :76-82
-    fl |= echo_send ? (F_EEX | F_ES) : 0u;
+    // a send the node already made (a user-issued ECHO / READY, base/broadcast.py:17) is a duplicate
+    // on every link: the state changes, the sender-identity network carries nothing new
+    const bool es_st = open && s_arr && !(fl & F_EEX);                      // :76-82
+    echo_send = es_st && !(fl & F_ES);
+    fl |= es_st ? (F_EEX | F_ES) : 0u;
     const bool e_on = open && ea != 0;
     const uint32_t checked = (fl & F_EEX) ? ea : ea - 1u;                   // :87-89
     fl |= e_on ? F_EEX : 0u;
     ec += e_on ? ea : 0u;                                                   // :89/:92
-    const bool r1 = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX); // :95-98
-    fl |= r1 ? (F_REX | F_RS) : 0u;
+    const bool r1s = e_on && checked != 0 && ec >= T_echo && !(fl & F_REX); // :95-98
+    const bool r1 = r1s && !(fl & F_RS);
+    fl |= r1s ? (F_REX | F_RS) : 0u;
     const bool r_on = open && ra != 0;
     const bool rex = (fl & F_REX) != 0;
     const uint32_t lo = rex ? rc + 1u : 2u, hi = rex ? rc + ra : ra;       // :103-108
@@ -1031,8 +1035,9 @@ void brc_step(const Params* __restrict__ pp) {
                 if (tbu & TB_S) {                                                // :76-82
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
-                        es[i] = (opn[i] ? sa[i] : 0u) & ~fl[i] & 1u;             // SEND, no ECHO entry
-                        fl[i] |= es[i] | (es[i] << 3);                           // F_EEX | F_ES
+                        const uint32_t est = (opn[i] ? sa[i] : 0u) & ~fl[i] & 1u;  // SEND, no ECHO entry
+                        es[i] = est & ~(fl[i] >> 3);                             // not sent already (user ECHO)
+                        fl[i] |= est | (est << 3);                               // F_EEX | F_ES
                     }
                 }
                 if (tbu & TB_E) {                                                // :84-98
@@ -1044,8 +1049,8 @@ void brc_step(const Params* __restrict__ pp) {
                         fl[i] |= eon;                                            // F_EEX
                         ec[i] += e;
                         const uint32_t r1 = eon & chk & ge(ec[i], T_echo) & (~fl[i] >> 1) & 1u;   // !F_REX (:95)
+                        rs[i] = r1 & ~(fl[i] >> 4);                              // not sent already (user READY)
                         fl[i] |= (r1 << 1) | (r1 << 4);                          // F_REX | F_RS
-                        rs[i] = r1;
                     }
                 }
                 if (tbu & TB_R) {                                                // :100-119
@@ -1201,6 +1206,7 @@ void brc_step(const Params* __restrict__ pp) {
             bool es, rs, dl;
             uint32_t n_ready = 0;                                // CONN: READY broadcasts this step
             bool first_ready = false;
+            const bool had_es = (fl & F_ES) != 0;                // a user-issued ECHO was logged already
             if constexpr (CONN) {
                 brb_cell_update_conn(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, n_ready, dl);
                 rs = n_ready != 0;
@@ -1234,7 +1240,7 @@ void brc_step(const Params* __restrict__ pp) {
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
-                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if (es && !had_es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
                 if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }

@@ -754,6 +754,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             bool es, rs, dl;
             uint32_t n_ready = 0;                                // CONN: READY broadcasts this step
             bool first_ready = false;
+            const bool had_es = (fl & F_ES) != 0;                // a user-issued ECHO was logged already
             if constexpr (CONN) {
                 brb_cell_update_conn(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, n_ready, dl);
                 rs = n_ready != 0;
@@ -784,7 +785,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             if (dl) s_dpos[(pos >> 6) * NPAD + d] |= 1ull << (pos & 63);   // pos: in this pass
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
-                if (es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if (es && !had_es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
                 if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }

@@ -36,11 +36,12 @@ def _workloads():
     W = {
         "ref-slow64": dict(base, n=64, f=21, seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8, round_cap=1,
                            key_window=4),
-        # multi-round reference consensus under slow-set D = 8 outgrows any phase window <= 8: fast
-        # replicas cycle rounds while their old keys still reach slow ones -- both kernels stop with
-        # BRC_OVERFLOW at the same step; constant delays run many rounds in Q = 8
-        "ref-slow64-r3-ovf": dict(base, n=64, f=21, seed=0x5EED0014, delay_model=L.DELAY_SLOWSET, delay_max=8,
-                                  round_cap=3, key_window=8),
+        "ref-slow64-r3": dict(base, n=64, f=21, seed=0x5EED0014, delay_model=L.DELAY_SLOWSET, delay_max=8,
+                              round_cap=3, key_window=8),
+        # reference consensus with delay 1 everywhere advances several phases per step: the phase
+        # window overflows (both kernels stop with BRC_OVERFLOW at the same step)
+        "ref-const64-cap30-ovf": dict(base, n=64, f=21, seed=0x5EED0034, delay_model=L.DELAY_CONST, delay_max=1,
+                                      delay_const=1, round_cap=0, key_window=8, step_cap=30),
         "ref-const64-r4": dict(base, n=64, f=21, seed=0x5EED0015, delay_model=L.DELAY_CONST, delay_max=2, delay_const=2,
                                round_cap=4, key_window=8),
         "spec-slow64": dict(base, n=64, f=21, seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8, round_cap=2,
@@ -57,9 +58,10 @@ def _workloads():
                               key_window=4),
         "spec-nv2-slow48": dict(base, n=48, f=15, seed=0x4802, delay_model=L.DELAY_SLOWSET, delay_max=4, round_cap=2,
                                 key_window=4, variants=2, mode=L.MODE_SPEC, coin_seed=COIN),
-        # round_cap 0: consensus runs on until the step cap (statistics truncated at step 30)
-        "ref-const64-cap30": dict(base, n=64, f=21, seed=0x5EED0034, delay_model=L.DELAY_CONST, delay_max=1,
-                                  delay_const=1, round_cap=0, key_window=8, step_cap=30),
+        # round_cap 0: consensus runs on until the step cap (statistics truncated at step 30, while keys
+        # created before it still have arrivals past it)
+        "ref-slow64-cap30": dict(base, n=64, f=21, seed=0x5EED0034, delay_model=L.DELAY_SLOWSET, delay_max=8,
+                                 round_cap=0, key_window=8, step_cap=30),
         # connection-identity peers (core/brbroadcast.py:69): the kernel's default use
         "conn-slow64": dict(base, n=64, f=21, seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8, round_cap=1,
                             key_window=4, peer_mode=L.PEER_CONNECTION),

@@ -27,7 +27,7 @@ INJ_PROPOSE, INJ_SEND, INJ_KEY, INJ_MSG, INJ_DELIVER = 1, 2, 3, 4, 5
 RUNNING, DONE, QUIESCENT, STEPCAP, OVERFLOW, BADINJ = 0, 1, 2, 3, 4, 5
 STATUS_NAMES = {RUNNING: "running", DONE: "done", QUIESCENT: "quiescent", STEPCAP: "stepcap",
                 OVERFLOW: "overflow", BADINJ: "bad_injection"}
-EV_DELIVER, EV_DECIDE, EV_SEND = 1, 2, 3
+EV_DELIVER, EV_DECIDE, EV_SEND, EV_COPY = 1, 2, 3, 4
 KERNEL_STEP, KERNEL_LIFE = 0, 1
 
 EXPORTS = ["brc_create", "brc_load_proposals", "brc_load_byzantine", "brc_inject", "brc_run",

@@ -599,10 +599,11 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     // slot generations are 13-bit (wide kernel 11-bit) tags: past the budget a stale cell could
     // read as current.  brc_reset clears fully once the budget is spent; a run that keeps stepping
     // one simulation without resetting must stop here instead of risking the wrap.
-    // The lean (compact-cell) kernels and the lifetime kernel keep no generation tags: a slot's row is
-    // rewritten at allocation, so only the 14-bit phase-index snapshot bounds them.
-    const uint64_t gen_hard = (e->wide ? GEN_MASK_W : GEN_MASK) - 2;
-    if (!e->compact && e->gen_base + 2 >= gen_hard) {
+    // The lean (compact-cell) kernels, the wide kernel and the lifetime kernel keep no generation tags:
+    // a slot's row is rewritten at allocation, so only the 14-bit phase-index snapshot bounds them.
+    const uint64_t gen_hard = GEN_MASK - 2;
+    const bool genfree = e->compact || e->wide;    // no cell generation tags (rows rewritten at allocation)
+    if (!genfree && e->gen_base + 2 >= gen_hard) {
         e->err = "slot generation budget exhausted: call brc_reset";
         return BRC_E_STATE;
     }
@@ -633,7 +634,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.mode = c.mode; P.coin_seed = c.coin_seed;
     // a slot allocated for phase index s has been reallocated at most gen_base + s/Q + 1 times
     // (and phase indices stay below 2^14 - 1: the narrow kernel's consensus snapshot keeps s + 1 in 14 bits)
-    P.s_limit = e->compact ? 0x3FFEu : (uint32_t)std::min<uint64_t>(0x3FFEull, (gen_hard - 1 - e->gen_base) * c.key_window);
+    P.s_limit = genfree ? 0x3FFEu : (uint32_t)std::min<uint64_t>(0x3FFEull, (gen_hard - 1 - e->gen_base) * c.key_window);
     P.cells = e->cells; P.meta = e->meta; P.mgen = e->mgen; P.kdst = e->kdst;
     P.act = e->act; P.actany = e->actany; P.items = e->items;
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
@@ -662,7 +663,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipEventElapsedTime(&e->last_ms, e->ev0, e->ev1));
     unsigned long long gc[8];
     HIPCHK(e, hipMemcpy(gc, e->gcount, sizeof(gc), hipMemcpyDeviceToHost));
-    if (!e->compact) e->gen_cur = std::max<uint64_t>(e->gen_cur, gc[5] / c.key_window + 2);   // gc[5]: max phase index
+    if (!genfree) e->gen_cur = std::max<uint64_t>(e->gen_cur, gc[5] / c.key_window + 2);   // gc[5]: max phase index
     if (running_left) *running_left = (uint32_t)gc[6];   // counted by the step kernel
     return BRC_OK;
 }
@@ -671,7 +672,7 @@ int brc_reset(void* h) {
     Engine* e = static_cast<Engine*>(h);
     if (!e) return BRC_E_INVALID;
     HIPCHK(e, hipSetDevice(e->cfg.device));
-    const bool full = e->gen_base + e->gen_cur >= (e->wide ? GEN_FULL_CLEAR_W : GEN_FULL_CLEAR);
+    const bool full = e->gen_base + e->gen_cur >= GEN_FULL_CLEAR;
     if (!full) { e->gen_base += e->gen_cur; e->gen_cur = 0; }
     int rc = clear_state(e, full);   // full: gen_base = gen_cur = 0
     if (rc) return rc;

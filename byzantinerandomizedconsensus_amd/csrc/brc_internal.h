@@ -30,13 +30,10 @@ __host__ __device__ inline uint32_t gen32(uint16_t g) {
 __host__ __device__ constexpr uint32_t ring_steps(int dm) { return dm <= 8 ? 16u : 32u; }
 constexpr uint32_t STEP_LIMIT = 60000;
 constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
-constexpr uint32_t GEN_MASK_W = 0x7FF;      // wide kernel (n > 64): 11-bit cell generation
-constexpr uint32_t GEN_FULL_CLEAR_W = 1500;
 constexpr int CHUNK_W = 4;                  // wide kernel: keys whose ballots are exchanged per barrier
 #ifndef BRC_WIDE_DCW
 #define BRC_WIDE_DCW 4
 #endif
-constexpr uint32_t SQCAP = 4;               // wide kernel: SENDs one replica's consensus may start per step
 // wide kernel: delivery-bitmap words per receiver = key-list positions per pass / 64
 __host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw < BRC_WIDE_DCW ? nkw : BRC_WIDE_DCW; }
 constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
@@ -131,7 +128,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
 // meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 | consensus area |
-// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | sq[SQCAP][NPAD] u32 | gen[NK] u16 | klist[NK] u16 |
+// xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | sq[Q][NPAD] u8 | fresh[nkw] u64 | klist[NK] u16 |
 // red[12] u32 | pmw[2][CHUNK_W][NW] u32
 // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32 (one key variant per origin)
 __host__ __device__ inline uint32_t cons_words_wide(bool spec, uint32_t npad, uint32_t Q) {
@@ -154,7 +151,7 @@ __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32
     const uint32_t nw = (uint32_t)npad / 64;
     return 8 * (NK + TS * nkw + dpos_words_wide(nkw) * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
                 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
-           4 * SQCAP * (uint32_t)npad + 2 * (NK + NK) + 4 * (12 + 2 * CHUNK_W * nw);
+           Q * (uint32_t)npad + 8 * nkw + 2 * NK + 4 * (12 + 2 * CHUNK_W * nw);
 }
 
 // Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of

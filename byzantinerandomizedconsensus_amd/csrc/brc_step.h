@@ -789,7 +789,8 @@ void brc_step(const Params* __restrict__ pp) {
                                 ring = ring_put(ring, tl, t, c);
                                 mycells[ri] = ring.lo;
                                 mycells[ri + 64] = ring.hi;
-                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                                // the first broadcast of (node, type, key) is a SEND event, every later copy a COPY
+                                log_ev((wv & bit) ? BRC_EV_COPY : BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                                 wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                                 mycells[(size_t)k * (CW * 64)] = wv;
                                 st_msgs += n;
@@ -1240,8 +1241,15 @@ void brc_step(const Params* __restrict__ pp) {
                 atomicOr((unsigned long long*)&s_dbits[(k >> 6) * 64 + lane], dl ? (1ull << (k & 63)) : 0ull);
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
-                if (es && !had_es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
-                if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (es) log_ev(had_es ? BRC_EV_COPY : BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if constexpr (CONN) {
+                    // connection peers: every READY broadcast travels; the first of the key is a SEND
+                    // event, the :119 re-fires after it COPY events (one per broadcast)
+                    for (uint32_t c = 0; c < n_ready; ++c)
+                        log_ev((c == 0 && first_ready) ? BRC_EV_SEND : BRC_EV_COPY, d, BRC_READY, kp, s, m_value(m));
+                } else if (rs) {
+                    log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                }
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends: ring marks at t + every delay some sending lane has; t_quiet of the key

@@ -16,7 +16,7 @@
 // keeps its links' delay CODES as NPL bit planes in registers (n bits per plane) and rebuilds the
 // mask of one delay with NPL ANDs per 64-bit word when a ballot word is non-zero.
 //
-// Cell word (one u64 per (receiver, key)): flags:5 | |E|:8 | |R|:8 | gen:11 | t_echo_sent:16 |
+// Cell word (one u64 per (receiver, key)): flags:5 | |E|:8 | |R|:8 | (unused):11 | t_echo_sent:16 |
 // t_ready_sent:16.  |E| saturates at 255 (only |E| >= T_echo <= 171 is ever tested) and |R| is
 // below T_del until the cell delivers, after which it is never read (core/brbroadcast.py:74).
 //
@@ -28,6 +28,12 @@
 #include "brc_step.h"
 
 namespace brc {
+
+// waves per SIMD the register allocation must allow (<= 168 VGPRs at 3): with generation-free cells
+// and a byte-wide SEND queue a cfg5 workgroup takes 48-51 KB of LDS, so three fit a CU
+#ifndef BRC_WIDE_WAVES
+#define BRC_WIDE_WAVES 3
+#endif
 
 
 __device__ __forceinline__ uint64_t wave_or64(uint64_t x) {
@@ -42,7 +48,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 }
 
 template <int NPAD, int DM, bool EV, int MODE>
-__global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restrict__ pp) {
+__global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     // u64 words per cell: CONN adds the lane's ECHO and READY send-count rings (Ring16, brc_step.h)
@@ -69,8 +75,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     const bool planes = !CONN && plane_model(model);
     const uint32_t nX = CONN ? 8u * nL : planes ? (uint32_t)NPL + 1u : nL;   // exchanged words per (key, type)
     // LDS carve (lds_bytes_wide): meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 |
-    //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | sq[SQCAP][NPAD] u32 |
-    //   gen[NK] u16 | klist[NK] u16 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
+    //   consensus area | xb[2][CHUNK_W][nX][2][NW] u64 | outm[16][NW] u64 | sq[Q][NPAD] u8 |
+    //   fresh[nkw] u64 | klist[NK] u16 | red[3][4] u32 | pmw[2][CHUNK_W][NW] u32
     // dpos: this pass's deliveries, one bit per key-list POSITION (not per key slot): a step's keys
     // are processed in passes of at most 64 DCW keys, which bounds the delivery bitmap (a slot-
     // indexed one would take NK x NPAD bits and cap the CU at one workgroup)
@@ -86,9 +92,11 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     uint32_t* s_cnt = (uint32_t*)s_hm;
     uint64_t* s_xb = s_hm + cons_words_wide(SPEC, NPAD, Q);
     uint64_t* s_outm = s_xb + 2 * CHUNK_W * nX * 2 * NW;
-    uint32_t* s_sq = (uint32_t*)(s_outm + 16 * NW);    // deferred SENDs: (phase index << 8 | value)
-    uint16_t* s_gen = (uint16_t*)(s_sq + SQCAP * NPAD);  // 11-bit generations
-    uint16_t* s_klist = s_gen + NK;                    // key slots < 2^11
+    uint8_t* s_sq = (uint8_t*)(s_outm + 16 * NW);      // deferred SENDs: values (phase indices consecutive)
+    // key slots (re)allocated since the last clear: their rows are rewritten "never sent" before
+    // anything reads them, so cells carry no generation tag (clear_fresh)
+    uint64_t* s_fresh = (uint64_t*)(s_sq + Q * NPAD);
+    uint16_t* s_klist = (uint16_t*)(s_fresh + nkw);    // key slots < 2^11
     uint32_t* s_red = (uint32_t*)(s_klist + NK);       // NK is a multiple of 64: 4-B aligned
     uint32_t* s_pmw = s_red + 12;                // per wave: delays (compact index) with any send
     const uint32_t d = (uint32_t)tid;
@@ -101,10 +109,9 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     ItemState its = P.items[inst];
     uint32_t t = its.t, inj_pos = its.inj_pos;
     const uint32_t inj_off = gp(P.inj_off)[inst], inj_cnt = gp(P.inj_cnt)[inst];
-    for (uint32_t i = d; i < NK; i += NPAD) {
-        s_meta[i] = gp(P.meta)[inst * NK + i];
-        s_gen[i] = (uint16_t)gp(P.mgen)[inst * NK + i];
-    }
+    for (uint32_t i = d; i < NK; i += NPAD)   // restricted-SEND flag in bit 63 of the LDS copy (value ids < 4)
+        s_meta[i] = gp(P.meta)[inst * NK + i] | ((gp(P.mgen)[inst * NK + i] & GEN_RESTRICTED) ? M_RESTRICTED : 0ull);
+    if (d < nkw) s_fresh[d] = 0;
     for (uint32_t i = d; i < TS * nkw; i += NPAD) s_act[i] = gp(P.act)[inst * TS * nkw + i];
     for (uint32_t w = 0; w < DCW; ++w) s_dpos[w * NPAD + d] = 0;
     for (uint32_t i = d; i < 16 * NW; i += NPAD) s_outm[i] = 0;
@@ -295,7 +302,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
         const uint64_t m = s_meta[k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
-        s_gen[k] = (uint16_t)(((s_gen[k] & GEN_MASK_W) + 1) & GEN_MASK_W);
+        atomicOr((unsigned long long*)&s_fresh[k >> 6], 1ull << (k & 63));   // the row is rewritten (clear_fresh)
         s_meta[k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
@@ -306,17 +313,31 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     // Consensus runs between key-list passes, so the SENDs it starts are queued and performed after
     // the step's last pass: every BRB message of the step (those of a key whose slot a new key
     // reuses included) is processed before any slot is reallocated, as the serial semantics have it.
-    uint32_t nsq = 0;
+    // One replica's SENDs of one step take distinct slots (phase index mod Q), so Q entries hold all
+    // of them: a (Q+1)-th would find its slot busy and overflow in send_key as well (a replica that
+    // starts late completes up to Q buffered SPEC phases at once).
+    // The SENDs of one replica in one step have consecutive phase indices (each phase change
+    // advances the index by one), so the queue keeps the first index and one value byte per SEND.
+    uint32_t nsq = 0, sq_s = 0;
     auto send_later = [&](uint32_t s, uint32_t v) {
-        if (nsq < SQCAP) s_sq[nsq++ * NPAD + d] = (s << 8) | (v & 0xFF);
-        else ovf = true;                      // more phase transitions of one replica in one step
+        if (nsq == 0) sq_s = s;
+        if (nsq < Q && s == sq_s + nsq) s_sq[nsq++ * NPAD + d] = (uint8_t)v;
+        else ovf = true;
     };
     auto flush_sends = [&]() {
-        for (uint32_t i = 0; i < nsq; ++i) {
-            const uint32_t e = s_sq[i * NPAD + d];
-            send_key(e >> 8, e & 0xFF);
-        }
+        for (uint32_t i = 0; i < nsq; ++i) send_key(sq_s + i, s_sq[i * NPAD + d]);
         nsq = 0;
+    };
+    // rewrite the rows of the slots allocated since the last call to "never sent" (each thread its
+    // own cell; the connection-peer send rings are ignored while the cell reads never sent)
+    auto clear_fresh = [&]() {
+        __syncthreads();
+        for (uint32_t w = 0; w < nkw; ++w)
+            for (uint64_t x = s_fresh[w]; x; x &= x - 1)
+                mycells[(size_t)(w * 64 + (uint32_t)__builtin_ctzll(x)) * (CW * NPAD)] = TIMES_NEVER;
+        __syncthreads();
+        if (d < nkw) s_fresh[d] = 0;
+        __syncthreads();
     };
     auto popc_hm = [&](uint32_t v) -> uint32_t {
         uint32_t c = 0;
@@ -412,6 +433,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                 send_key(0, v & 3);
                 if constexpr (SPEC) spec_advance(false);              // phase 0 may be buffered
             }
+            clear_fresh();
         }
         while (inj_pos < inj_cnt) {
             const InjDev r = load_inj(P.inj + inj_off + inj_pos);
@@ -443,17 +465,15 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                     const uint32_t k = r.slot;
                     if (d == 0) {
                         uint64_t m = s_meta[k];
-                        uint32_t gen = s_gen[k] & GEN_MASK_W;
                         const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
                         if ((!declared && m_s1(m) != 0 && t < m_tquiet(m)) || r.s >= P.s_limit) {
                             ovf = true;
                         } else {
                             uint32_t tq = m_tquiet(m);
-                            if (!declared) { gen = (gen + 1) & GEN_MASK_W; tq = t + 1; }
+                            if (!declared) { tq = t + 1; s_fresh[k >> 6] |= 1ull << (k & 63); }
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
-                            s_meta[k] = m;
-                            s_gen[k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
+                            s_meta[k] = m | (restricted ? M_RESTRICTED : 0ull);
                             st_smax = max(st_smax, (uint32_t)r.s);
                             if (is_send) {
                                 mark_lane(k, os);
@@ -479,9 +499,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                     if (m_s1(m) != r.s + 1u) {
                         badinj = true;
                     } else {
-                        const uint32_t gen = s_gen[k] & GEN_MASK_W;
                         uint64_t wv = mycells[(size_t)k * (CW * NPAD)];
-                        if (((wv >> 21) & GEN_MASK_W) != gen) wv = TIMES_NEVER | ((uint64_t)gen << 21);
                         const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
                         const int sh = (r.type == BRC_ECHO) ? 32 : 48;
                         if constexpr (CONN) {
@@ -497,7 +515,8 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                                 ring = ring_put(ring, tl, t, c);
                                 rp[0] = ring.lo;
                                 rp[NPAD] = ring.hi;
-                                if (!(wv & bit)) log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                                // the first broadcast of (node, type, key) is a SEND event, every later copy a COPY
+                                log_ev((wv & bit) ? BRC_EV_COPY : BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
                                 wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
                                 mycells[(size_t)k * (CW * NPAD)] = wv;
                                 st_msgs += n;
@@ -522,6 +541,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                     }
                 }
             }
+            if (r.kind != BRC_INJ_MSG) clear_fresh();    // PROPOSE / DELIVER / SEND / KEY may allocate a slot
         }
         its.initialized = 1;
         return mine_any;
@@ -586,16 +606,14 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
         // The key id, meta word and generation it reads stay in SGPRs for phase 2 (process): meta
         // changes in between only in t_quiet, through process's own atomicMax, which keeps the max.
         auto ballots = [&](uint32_t p, uint32_t buf, const uint64_t (&ww)[CHUNK_W], const uint32_t (&kk)[CHUNK_W],
-                           uint64_t (&mm)[CHUNK_W], uint32_t (&gg)[CHUNK_W]) {
+                           uint64_t (&mm)[CHUNK_W]) {
             Unrolled<CHUNK_W>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 if (p + c < nkeys) {
                     const uint32_t k = kk[c];
                     const uint64_t m = uni64(s_meta[k]);
-                    const uint32_t gw = uni32(s_gen[k]);
-                    mm[c] = m; gg[c] = gw;
-                    const uint32_t gen = gw & GEN_MASK_W;
-                    const bool cur = m_s1(m) != 0 && real && (((uint32_t)ww[c] >> 21) & GEN_MASK_W) == gen;
+                    mm[c] = m;
+                    const bool cur = m_s1(m) != 0 && real;
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
                     uint64_t* xb = s_xb + ((buf * CHUNK_W + c) * nX) * 2 * NW;
@@ -660,11 +678,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             });
         };
         // phase 2: one (receiver d, key k) cell
-        auto process = [&](const uint32_t k, const uint64_t wd, const uint64_t m, const uint32_t gw, uint32_t buf, int c,
+        auto process = [&](const uint32_t k, const uint64_t wd, const uint64_t m, uint32_t buf, int c,
                            uint32_t pos) __attribute__((always_inline)) {
-            const uint32_t gen = gw & GEN_MASK_W;
             const bool kl = m_s1(m) != 0;                        // the slot holds a key
-            const bool cur = kl && real && (((uint32_t)wd >> 21) & GEN_MASK_W) == gen;
+            const bool cur = kl && real;
             const uint64_t word = cur ? wd : TIMES_NEVER;
             const uint32_t tE = (uint32_t)(word >> 32) & 0xFFFF, tR = (uint32_t)(word >> 48);
             uint32_t ea = 0, ra = 0;
@@ -745,7 +762,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             const bool s_win = kl && dt - 1u < D && ((dset >> ((dt - 1u) & 31)) & 1u);   // uniform
             if (s_win) {
                 bool hit = link_delay(m_sender(m)) == dt;
-                if (gw & GEN16_RESTRICTED) hit = hit && ((gp(P.kdst)[(inst * NK + k) * NW + wid] >> lane) & 1ull);
+                if (m & M_RESTRICTED) hit = hit && ((gp(P.kdst)[(inst * NK + k) * NW + wid] >> lane) & 1ull);
                 s_arr = honest && hit;
             }
             const bool has = kl && honest && (s_arr || ea || ra);
@@ -775,7 +792,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             {
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)min(ec, 255u) << 5) | ((uint64_t)min(rc, 255u) << 13) |
-                                    ((uint64_t)gen << 21) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+                                    ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
                 mycells[(size_t)k * (CW * NPAD)] = has ? nw : wd;
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
@@ -785,8 +802,15 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             if (dl) s_dpos[(pos >> 6) * NPAD + d] |= 1ull << (pos & 63);   // pos: in this pass
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
-                if (es && !had_es) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
-                if (CONN ? first_ready : rs) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                if (es) log_ev(had_es ? BRC_EV_COPY : BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));
+                if constexpr (CONN) {
+                    // connection peers: every READY broadcast travels; the first of the key is a SEND
+                    // event, the :119 re-fires after it COPY events (one per broadcast)
+                    for (uint32_t c = 0; c < n_ready; ++c)
+                        log_ev((c == 0 && first_ready) ? BRC_EV_SEND : BRC_EV_COPY, d, BRC_READY, kp, s, m_value(m));
+                } else if (rs) {
+                    log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m));
+                }
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
             // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
@@ -820,15 +844,14 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
                 for (uint32_t p = base; p < end; p += CHUNK_W) {
                     const uint32_t buf = (p / CHUNK_W) & 1;
                     uint64_t mA[CHUNK_W];
-                    uint32_t gA[CHUNK_W];
-                    ballots(p, buf, wA, kA, mA, gA);
+                    ballots(p, buf, wA, kA, mA);
                     __syncthreads();
                     uint64_t wB[CHUNK_W];
                     uint32_t kB[CHUNK_W];
                     fetch(p + CHUNK_W, wB, kB);
                     Unrolled<CHUNK_W>::run([&](auto ci) {
                         constexpr int c = decltype(ci)::value;
-                        if (p + c < end) process(kA[c], wA[c], mA[c], gA[c], buf, c, p + c - base);
+                        if (p + c < end) process(kA[c], wA[c], mA[c], buf, c, p + c - base);
                     });
                     Unrolled<CHUNK_W>::run([&](auto ci) {
                         constexpr int c = decltype(ci)::value;
@@ -859,6 +882,7 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
             __syncthreads();
         }
         flush_sends();
+        clear_fresh();
 
         // ================= actions stamped t
         const bool inj_mine = do_actions();
@@ -880,7 +904,10 @@ __global__ __launch_bounds__(NPAD, 1) void brc_step_wide(const Params* __restric
     __syncthreads();
 
     // ---- write back
-    for (uint32_t i = d; i < NK; i += NPAD) { gp(P.meta)[inst * NK + i] = s_meta[i]; gp(P.mgen)[inst * NK + i] = s_gen[i]; }
+    for (uint32_t i = d; i < NK; i += NPAD) {
+        gp(P.meta)[inst * NK + i] = s_meta[i] & ~M_RESTRICTED;
+        gp(P.mgen)[inst * NK + i] = (s_meta[i] & M_RESTRICTED) ? GEN_RESTRICTED : 0u;
+    }
     for (uint32_t i = d; i < TS * nkw; i += NPAD) gp(P.act)[inst * TS * nkw + i] = s_act[i];
     if (d == 0) {
         gp(P.actany)[inst] = any_rows;

@@ -20,7 +20,7 @@ by hand) into ``Engine.inject`` records.  Pure host code: no engine calls.
 import json
 
 SEND, ECHO, READY = 1, 2, 3
-EV_SEND = 3
+EV_SEND, EV_COPY = 3, 4
 DEFAULT_VALUES = ("-1", "0", "1", "3")
 
 
@@ -89,17 +89,15 @@ class Codec:
         events: ``Engine.events()`` tuples (instance, t, kind, node, type, kp, s, value id).
         dst_masks: {(t, node, type, kp, s): destination bit mask} for sends that did not go to
         every peer (the Byzantine injections that were restricted); everything else went to all.
+        Connection-identity peers (core/brbroadcast.py:69) put every broadcast on the wire, the
+        :119 READY re-fires included: the engine logs each one after the first as an EV_COPY
+        event, and each becomes one more envelope per peer.
         """
-        if self.peer_mode == "connection":
-            # connection-identity peers (core/brbroadcast.py:69): the :119 amplification re-sends
-            # READY once per qualifying READY, and the event log -- like the reference harness's
-            # send log -- records a broadcast only the first time, so the copies are not there
-            raise ValueError("wire export needs sender-identity peers: a connection-identity run re-sends "
-                             "READY copies that its event log records once")
         allm = (1 << self.n) - 1
+        kinds = (EV_SEND, EV_COPY) if self.peer_mode == "connection" else (EV_SEND,)
         out = []
         for (inst, t, kind, node, typ, kp, s, value) in events:
-            if inst != instance or kind != EV_SEND:
+            if inst != instance or kind not in kinds:
                 continue
             env = envelope(self.addrs[node][0], typ, self.payload(kp, s, value))
             mask = (dst_masks or {}).get((t, node, typ, kp, s), allm)

@@ -71,7 +71,11 @@ enum { BRC_SEND = 1, BRC_ECHO = 2, BRC_READY = 3 };
  * protocol, BRC_MODE_REFERENCE or BRC_MODE_BEB (BRC_MODE_SPEC counts phases: BRC_E_UNSUPPORTED). */
 enum { BRC_INJ_PROPOSE = 1, BRC_INJ_SEND = 2, BRC_INJ_KEY = 3, BRC_INJ_MSG = 4, BRC_INJ_DELIVER = 5 };
 enum { BRC_RUNNING = 0, BRC_DONE = 1, BRC_QUIESCENT = 2, BRC_STEPCAP = 3, BRC_OVERFLOW = 4, BRC_BADINJ = 5 };
-enum { BRC_EV_DELIVER = 1, BRC_EV_DECIDE = 2, BRC_EV_SEND = 3 };
+/* BRC_EV_SEND: the first broadcast of (node, type, key) -- the reference harness's send log.
+ * BRC_EV_COPY (connection-identity peers only): every later broadcast of it, one event each (the
+ * :119 READY re-fires, repeated injected messages); with the SEND events they are the complete wire
+ * traffic (wire.Codec.export).  Sender-identity peers suppress such duplicates on the network. */
+enum { BRC_EV_DELIVER = 1, BRC_EV_DECIDE = 2, BRC_EV_SEND = 3, BRC_EV_COPY = 4 };
 
 typedef struct {
     uint32_t n;               /* replicas per instance, self included (1..256) */

@@ -94,7 +94,7 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
             per[inst]["deliver"].append([t, node, a, b])
         elif kind == L.EV_DECIDE:
             per[inst]["decide"].append([t, node, a, specs[inst]["values"][b]])
-        else:
+        elif kind == L.EV_SEND:                # first broadcasts (copies: L.EV_COPY, wire export only)
             per[inst]["send"].append([t, node, typ, a, b])
     out = []
     for i, sp in enumerate(specs):

@@ -90,7 +90,12 @@ def wire_specs():
     """Small runs whose every wire message (the bytes base/broadcast.py:37-38 puts on a TCP
     connection) is kept: BRB, consensus, and a Byzantine equivocator."""
     G = S.scenario_groups()
-    return [G["brb_fifo_n4"][0], G["cons_brc_test_n6"][0], G["cons_uniform_n4"][0], G["brb_byz_n7"][0]]
+    K = {sp["name"]: sp for sp in G["conn_kat"]}
+    # connection-identity peers (core/brbroadcast.py:69): every broadcast is on the wire, the :119
+    # READY re-fires (K4, K12) and repeated Byzantine messages (K5) included
+    return [G["brb_fifo_n4"][0], G["cons_brc_test_n6"][0], G["cons_uniform_n4"][0], G["brb_byz_n7"][0],
+            G["conn_brb_fifo_n4"][0], G["conn_cons_brc_test_n6"][0], K["K4-conn"], K["K5-conn"], K["K12-conn"],
+            G["conn_brb_usermsg_n7"][1]]
 
 
 def write_wire():

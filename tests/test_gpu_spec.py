@@ -106,3 +106,23 @@ def test_round_histogram_vs_oracle():
         got = eng.round_histogram(bins)
     assert got == exp
     assert sum(exp[2:]) > 0, "some instance needed a coin round"
+
+
+@pytest.mark.parametrize("n,f", [(70, 23), (100, 33), (48, 15)])
+def test_spec_late_replica_completes_buffered_phases_at_once(runner, n, f):
+    """A replica that proposes late finds Q phases' deliveries buffered and completes them in ONE
+    step: up to Q = 8 SENDs by one replica in one step (the wide kernel queues them until the step's
+    last key pass).  Start steps 14 / 18 / 22 give 5 / 7 / 8 such SENDs (checked below)."""
+    import collections
+    specs = []
+    for j, ts in enumerate((14, 18, 22)):
+        starts = [0] * n
+        starts[n - 1] = ts
+        sp = S.spec_cons_spec(n, f, 0x5EED0106, 0, 1, j, round_cap=3, window=8, coin_seed=0xC017C017,
+                              starts=starts)
+        sp["name"] = "speclate%d/%d" % (n, ts)
+        specs.append(sp)
+    got = _compare(runner, specs)
+    bursts = [max(collections.Counter((t, src) for t, src, typ, _kp, _s in r["events"]["send"] if typ == 1).values())
+              for r in got]
+    assert max(bursts) >= 7 and all(r["status"] == "done" for r in got), bursts

@@ -10,12 +10,14 @@ pytestmark = pytest.mark.gpu
 
 
 def run_events(spec, injections):
+    from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd.engine import Engine
     with Engine(n=spec["n"], f=spec["f"], instances=1, protocol=spec["mode"], seed=spec["seed"],
                 delay_model=spec["delay_model"], delay_max=spec["dmax"], delay_const=spec.get("dconst", 1),
                 round_cap=spec.get("round_cap", 0), step_cap=spec.get("step_cap", 10000),
                 key_window=8 // spec.get("nv", 1), variants=spec.get("nv", 1),
-                byzantine=spec.get("byzantine", ()), event_capacity=1 << 20, instance_offset=spec["g"]) as eng:
+                byzantine=spec.get("byzantine", ()), event_capacity=1 << 20, instance_offset=spec["g"],
+                peer_mode=L.PEER_CONNECTION if spec.get("peer_mode") == "connection" else L.PEER_SENDER) as eng:
         eng.inject(injections)
         eng.run()
         return eng.events(), eng.instances_result()[0]

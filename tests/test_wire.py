@@ -24,7 +24,7 @@ CASES = load_cases()
 def codec_for(spec):
     payloads = {(a["kp"], a["s"]): a["payload"] for a in spec["actions"] if "payload" in a}
     return wire.Codec(spec["n"], mode=spec["mode"], nv=spec.get("nv", 1), values=spec["values"],
-                      payloads=payloads)
+                      payloads=payloads, peer_mode=spec.get("peer_mode", "sender"))
 
 
 def dst_masks(spec):
@@ -62,12 +62,21 @@ def test_byzantine_traffic_becomes_its_injections():
     assert norm(got) == norm(want)
 
 
-def test_export_refuses_connection_identity_logs():
-    # a connection-identity run (core/brbroadcast.py:69) re-sends READY copies (:119) that the
-    # event log records once: exporting it as the complete wire would drop messages
-    from byzantinerandomizedconsensus_amd import wire
+def test_connection_export_counts_every_broadcast():
+    # connection-identity peers (core/brbroadcast.py:69): a READY re-fire (:119) is logged as a COPY
+    # event and exported as one more envelope per peer; sender peers never carry copies
     c = wire.Codec(4, peer_mode="connection")
-    with pytest.raises(ValueError):
-        c.export([(0, 1, wire.EV_SEND, 0, wire.SEND, 0, 0, 1)])
+    evs = [(0, 1, wire.EV_SEND, 2, wire.READY, 0, 0, 1), (0, 2, wire.EV_COPY, 2, wire.READY, 0, 0, 1),
+           (0, 2, wire.EV_COPY, 2, wire.READY, 0, 0, 1)]
+    assert len(c.export(evs)) == 12
+    assert len(wire.Codec(4).export(evs)) == 4
     with pytest.raises(ValueError):
         wire.Codec(4, peer_mode="tcp")
+
+
+def test_connection_cases_carry_refires():
+    # the connection-identity fixtures hold more envelopes than first broadcasts x peers: re-fires
+    conn = [c for c in CASES if c["spec"].get("peer_mode") == "connection"]
+    assert len(conn) >= 4
+    firsts = {c["spec"]["name"]: c["result"]["counts"]["send"] * c["spec"]["n"] for c in conn}
+    assert any(len(c["wire"]) > firsts[c["spec"]["name"]] for c in conn)

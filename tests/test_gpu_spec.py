@@ -112,10 +112,12 @@ def test_round_histogram_vs_oracle():
 def test_spec_late_replica_completes_buffered_phases_at_once(runner, n, f):
     """A replica that proposes late finds Q phases' deliveries buffered and completes them in ONE
     step: up to Q = 8 SENDs by one replica in one step (the wide kernel queues them until the step's
-    last key pass).  Start steps 14 / 18 / 22 give 5 / 7 / 8 such SENDs (checked below)."""
+    last key pass).  Start steps 14 / 18 give 5 / 7 such SENDs (checked below); at 22 the
+    eighth would reuse the slot of the replica's own phase-0 key, which the engine's phase window
+    reports as BRC_OVERFLOW."""
     import collections
     specs = []
-    for j, ts in enumerate((14, 18, 22)):
+    for j, ts in enumerate((14, 18)):
         starts = [0] * n
         starts[n - 1] = ts
         sp = S.spec_cons_spec(n, f, 0x5EED0106, 0, 1, j, round_cap=3, window=8, coin_seed=0xC017C017,

@@ -109,10 +109,14 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 // key metadata), the others one untyped row.
 __host__ __device__ constexpr uint32_t act_types(bool lean) { return lean ? 2u : 1u; }
 
+// Injection records the non-lean narrow kernels stage in LDS at a time (one memory round trip per
+// INJ_CACHE records instead of one per record: cfg3's equivocation pattern is 120 records per wave)
+constexpr uint32_t INJ_CACHE = 16;
+
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][act_types][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u16 (not on the lean kernels) | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
-// reused as the consensus snapshot snap[IPW*NK] u16)
+// reused as the consensus snapshot snap[IPW*NK] u16) | injc[INJ_CACHE][3] u64 (not on the lean kernels)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
     const uint32_t ipw = 64 / (uint32_t)npad;
@@ -123,7 +127,9 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
-    return 8 * (ipw * NK + rs * nkw * act_types(lean) + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4);
+    const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;
+    return 8 * (ipw * NK + rs * nkw * act_types(lean) + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4 +
+                injc_words);
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):

@@ -340,6 +340,8 @@ void brc_step(const Params* __restrict__ pp) {
     // mid-loop (send_key), while another replica may still have to count a delivery of the old key
     // in that slot from this same step (its t_quiet may be this step): deliveries read the snapshot.
     uint16_t* s_snap = s_klist;
+    // non-lean kernels: a window of the item's injection records, staged in LDS (INJ_CACHE at a time)
+    uint64_t* s_injc = (uint64_t*)(s_klist + ((max(NK + 2 * CHUNK, IPW * NK) + 3) & ~3u));
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -354,6 +356,28 @@ void brc_step(const Params* __restrict__ pp) {
     uint32_t t = LEAN ? uni32(its.t) : its.t, inj_pos = LEAN ? uni32(its.inj_pos) : its.inj_pos;   // lean: wave-uniform
     uint32_t ep = LEAN ? uni32(its.epoch) : 0u;  // lean: compact-cell send steps are offsets from ep
     const uint32_t inj_off = gp(P.inj_off)[item], inj_cnt = gp(P.inj_cnt)[item];
+    // injection record `pos` of this item: lean kernels load it directly (their workloads carry few);
+    // the others keep INJ_CACHE records staged in LDS and refill the window with one coalesced load
+    uint32_t injc_base = 0x80000000u;           // no window yet: pos - injc_base >= INJ_CACHE for any pos
+    auto inj_at = [&](uint32_t pos) -> InjDev {
+        if constexpr (LEAN) {
+            return load_inj(P.inj + inj_off + pos);
+        } else {
+            if (pos - injc_base >= INJ_CACHE) {
+                injc_base = pos;
+                const uint32_t i = pos + (uint32_t)lane / 3u;
+                if ((uint32_t)lane < 3 * INJ_CACHE && i < inj_cnt)
+                    s_injc[lane] = gp((const uint64_t*)(P.inj + inj_off + i))[lane % 3];
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            const uint32_t o = 3 * (pos - injc_base);
+            const uint64_t w[3] = {s_injc[o], s_injc[o + 1], s_injc[o + 2]};
+            InjDev r;
+            __builtin_memcpy(&r, w, 24);
+            r.dst_hi[0] = r.dst_hi[1] = r.dst_hi[2] = 0;
+            return r;
+        }
+    };
     {
         const uint64_t mb = item * IPW * (uint64_t)NK;
         for (uint32_t i = lane; i < IPW * NK; i += 64) {
@@ -691,7 +715,7 @@ void brc_step(const Params* __restrict__ pp) {
             flush_clears();
         }
         while (inj_pos < inj_cnt) {
-            const InjDev r = load_inj(P.inj + inj_off + inj_pos);
+            const InjDev r = inj_at(inj_pos);
             if (r.t != t) break;
             ++inj_pos;
             const bool mine = running && seg == (int)r.seg;
@@ -853,7 +877,7 @@ void brc_step(const Params* __restrict__ pp) {
         const uint32_t rr = (rot ? ((any_rows >> rot) | (any_rows << (RS - rot))) : any_rows) &
                             (RS == 32 ? ~0u : ((1u << RS) - 1u));
         uint32_t next = rr ? t + (uint32_t)__ffs(rr) : 0xFFFFFFFFu;
-        if (inj_pos < inj_cnt) next = min(next, gp(P.inj)[inj_off + inj_pos].t);
+        if (inj_pos < inj_cnt) next = min(next, inj_at(inj_pos).t);
         if (next == 0xFFFFFFFFu) { if (running) status = BRC_QUIESCENT; break; }
         if (next > P.step_cap) { if (running) status = BRC_STEPCAP; break; }
         t = LEAN ? uni32(next) : next;
@@ -1485,16 +1509,17 @@ void brc_step(const Params* __restrict__ pp) {
         const uint64_t b_ovf = __ballot(ovf) & segbits;
         const uint64_t b_bad = __ballot(badinj) & segbits;
         const uint64_t b_und = __ballot(honest && dcount < P.round_cap) & segbits;
+        // segments with injections still to come (scanned by the whole wave: the record window is
+        // refilled with every lane active)
+        uint32_t seg_pending = 0;
+        if (__any(running && q_until <= t && inj_pos < inj_cnt))
+            for (uint32_t p = inj_pos; p < inj_cnt; ++p) seg_pending |= 1u << inj_at(p).seg;
         if (running) {
             if (b_act) t_stop = t;
             if (b_bad) status = BRC_BADINJ;
             else if (b_ovf) status = BRC_OVERFLOW;
             else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !b_und) status = BRC_DONE;
-            else if (q_until <= t) {
-                bool pending = false;
-                for (uint32_t p = inj_pos; p < inj_cnt && !pending; ++p) pending = gp(P.inj)[inj_off + p].seg == (uint32_t)seg;
-                if (!pending) status = BRC_QUIESCENT;
-            }
+            else if (q_until <= t && !((seg_pending >> seg) & 1u)) status = BRC_QUIESCENT;
         }
         if ((uint32_t)lane < nkw * AT) s_act[row * nkw * AT + lane] = 0;
         any_rows &= ~(1u << row);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Dev-only: per-section cycle split of the lean step kernel on the cfg4 workload.
+"""Dev-only: per-section cycle split of the narrow step kernel.
 Needs a variant built with -DBRC_STAMPS (tools/variant.py stamps -DBRC_STAMPS); run with
-BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances] [reference|spec]."""
+BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances] [reference|spec|<configs.py workload>]."""
 import ctypes
 import os
 import sys
@@ -11,16 +11,24 @@ from byzantinerandomizedconsensus_amd import _lib as L  # noqa: E402
 from byzantinerandomizedconsensus_amd.engine import Engine  # noqa: E402
 
 inst = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18
-spec = len(sys.argv) > 2 and sys.argv[2] == "spec"
-eng = Engine(n=64, f=21, instances=inst, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET,
-             delay_max=8, round_cap=1, step_cap=4000, key_window=8 if spec else 4, variants=1,
-             proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+which = sys.argv[2] if len(sys.argv) > 2 else "reference"
+os.environ["BRC_KERNEL"] = "step"
+if which in ("reference", "spec"):
+    spec = which == "spec"
+    eng = Engine(n=64, f=21, instances=inst, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET,
+                 delay_max=8, round_cap=1, step_cap=4000, key_window=8 if spec else 4, variants=1,
+                 proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+else:
+    import configs
+    _size, _per, kw = configs.workloads(L)[which]
+    eng = Engine(instances=inst, **kw)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
 out = (ctypes.c_ulonglong * 8)()
+dbg = lib.brc_dbg_stamps16 if eng.n <= 16 else lib.brc_dbg_stamps    # each unit keeps its own timers
 eng.reset(); eng.run()
-lib.brc_dbg_stamps(out)
+dbg(out)
 eng.reset(); eng.run()
-lib.brc_dbg_stamps(out)
+dbg(out)
 tot = sum(out[:4])
 names = ["step head + key list", "key loop (BRB cells)", "consensus deliveries", "actions + stop checks"]
 for nm, v in zip(names, out[:4]):

@@ -48,6 +48,7 @@ class ByzantineRandomizedConsensus(Consensus, IBroadcastHandler):
         consumed inside the engine; a direct call -- a JSON message as the reference builds it
         (:48-49), {"host": address, "round": r, "phase": p, "message": value} -- is handed to this
         replica's consensus state at the cluster's current step (round and phase are not read,
-        as in the reference)."""
+        as in the reference).  A non-string "message" or a host outside the peer list raises
+        EngineError (network.py's deviation notes)."""
         d = json.loads(message)
-        self.brb.cluster.deliver(self.brb.node_id, tuple(d["host"]), str(d["message"]))
+        self.brb.cluster.deliver(self.brb.node_id, tuple(d["host"]), d["message"])

@@ -11,8 +11,8 @@ int launch_step_16(int dm, bool events, int mode, uint32_t blocks, uint32_t lds,
 #ifdef BRC_STAMPS
 // dev-only: the section timers of this unit's kernels (tools/stamps.py, NPAD = 16 workloads)
 extern "C" int brc_dbg_stamps16(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(brc::brc_stamps), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(brc::brc_stamps), BRC_NSTAMPS * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[BRC_NSTAMPS] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(brc::brc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -33,8 +33,8 @@ int launch_step_64r(int dm, bool events, int mode, uint32_t blocks, uint32_t lds
 #ifdef BRC_STAMPS
 // dev-only: read and clear the section timers of the lean NPAD = 64 kernels (tools/stamps.py)
 extern "C" int brc_dbg_stamps(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(brc::brc_stamps), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(brc::brc_stamps), BRC_NSTAMPS * sizeof(unsigned long long)) != hipSuccess) return -1;
+    const unsigned long long z[BRC_NSTAMPS] = {};
     return hipMemcpyToSymbol(HIP_SYMBOL(brc::brc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -282,9 +282,10 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 // metadata read once per chunk, exec-masked cell stores and (NLR = 2) link-delay masks held in
 // registers -- the headline configuration has exactly two link delays.
 #ifdef BRC_STAMPS
-// dev-only: [0..3] section timers (s_memtime ticks); [4..7] lean key-steps: processed, without
+#define BRC_NSTAMPS 9
+// dev-only: [0..4] section timers (s_memtime ticks); [5..8] lean key-steps: processed, without
 // arrivals, reaching only delivered cells, fully updated
-__device__ unsigned long long brc_stamps[8];
+__device__ unsigned long long brc_stamps[BRC_NSTAMPS];
 #endif
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
 
@@ -700,6 +701,80 @@ void brc_step(const Params* __restrict__ pp) {
         spec_advance();
     };
 
+    // BRC_INJ_MSG: this lane (the record's node) broadcasts ECHO / READY of key r.slot; true if the
+    // message travels (sender peers: not a duplicate; connection peers: always)
+    auto msg_cell = [&](const InjDev& r) -> bool {
+        const uint32_t k = r.slot;
+        bool sent = false;
+        const uint64_t m = s_meta[mbase + k];
+        if (m_s1(m) != r.s + 1u) {
+            badinj = true;
+        } else if constexpr (LEAN) {
+            // compact cell: F_ES / F_RS and the send-step offset
+            const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
+            const uint32_t wv = *p;
+            const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
+            const uint32_t sh = (r.type == BRC_ECHO) ? C32_OE_SH : C32_OR_SH;
+            if (!(wv & bit)) {
+                sent = true;
+                *p = ((wv | bit) & ~(127u << sh)) | ((t - ep) << sh);
+                st_msgs += n;
+                log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+            }
+        } else {
+            const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
+            uint64_t wv = mycells[(size_t)k * (CW * 64)];
+            const bool stale = ((wv >> 19) & GEN_MASK) != gen;
+            if (stale) wv = TIMES_NEVER | ((uint64_t)gen << 19);
+            const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
+            const int sh = (r.type == BRC_ECHO) ? 32 : 48;
+            if constexpr (CONN) {
+                // every injected broadcast travels: one more send of this type at step t
+                const size_t ri = (size_t)k * (CW * 64) + ((r.type == BRC_ECHO) ? 64 : 192);
+                const uint32_t tl = (uint32_t)(wv >> sh) & 0xFFFF;
+                Ring16 ring = {mycells[ri], mycells[ri + 64]};
+                const uint32_t c = ring_count(ring, tl, t) + 1u;
+                if (c > RING_MAX) {
+                    badinj = true;                      // beyond the one-byte count
+                } else {
+                    sent = true;
+                    ring = ring_put(ring, tl, t, c);
+                    mycells[ri] = ring.lo;
+                    mycells[ri + 64] = ring.hi;
+                    // the first broadcast of (node, type, key) is a SEND event, every later copy a COPY
+                    log_ev((wv & bit) ? BRC_EV_COPY : BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                    wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                    mycells[(size_t)k * (CW * 64)] = wv;
+                    st_msgs += n;
+                }
+            } else if (!(wv & bit)) {
+                sent = true;
+                wv |= bit;
+                wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
+                mycells[(size_t)k * (CW * 64)] = wv;
+                st_msgs += n;
+                log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+            }
+        }
+        return sent;
+    };
+    // ... and its wave-level effects: ring marks at t + the senders' link delays, the key's t_quiet
+    auto msg_marks = [&](const InjDev& r, bool mine, bool sent) {
+        const uint32_t k = r.slot;
+        const uint32_t os = wave_or(sent ? outset : 0u);
+        if (os) {
+            if (lane == 0) mark_lane(k, os, r.type);
+            const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
+            if (mine && myq) {
+                if (d == 0) {
+                    const uint64_t m = s_meta[mbase + k];
+                    if (myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
+                }
+                q_until = max(q_until, myq);
+            }
+        }
+    };
+
     // ---- actions stamped t (performed after step t's messages)
     auto do_actions = [&]() -> bool {
         bool mine_any = false;
@@ -775,71 +850,38 @@ void brc_step(const Params* __restrict__ pp) {
                     q_until = max(q_until, t + hibit(os));
                 }
             } else if (r.kind == BRC_INJ_MSG) {
-                const uint32_t k = r.slot;
-                bool sent = false;
-                if (mine && d == r.node) {
-                    const uint64_t m = s_meta[mbase + k];
-                    if (m_s1(m) != r.s + 1u) {
-                        badinj = true;
-                    } else if constexpr (LEAN) {
-                        // compact cell: F_ES / F_RS and the send-step offset
-                        const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
-                        const uint32_t wv = *p;
-                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
-                        const uint32_t sh = (r.type == BRC_ECHO) ? C32_OE_SH : C32_OR_SH;
-                        if (!(wv & bit)) {
-                            sent = true;
-                            *p = ((wv | bit) & ~(127u << sh)) | ((t - ep) << sh);
-                            st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
-                        }
-                    } else {
-                        const uint32_t gen = s_gen[mbase + k] & GEN_MASK;
-                        uint64_t wv = mycells[(size_t)k * (CW * 64)];
-                        const bool stale = ((wv >> 19) & GEN_MASK) != gen;
-                        if (stale) wv = TIMES_NEVER | ((uint64_t)gen << 19);
-                        const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
-                        const int sh = (r.type == BRC_ECHO) ? 32 : 48;
-                        if constexpr (CONN) {
-                            // every injected broadcast travels: one more send of this type at step t
-                            const size_t ri = (size_t)k * (CW * 64) + ((r.type == BRC_ECHO) ? 64 : 192);
-                            const uint32_t tl = (uint32_t)(wv >> sh) & 0xFFFF;
-                            Ring16 ring = {mycells[ri], mycells[ri + 64]};
-                            const uint32_t c = ring_count(ring, tl, t) + 1u;
-                            if (c > RING_MAX) {
-                                badinj = true;                      // beyond the one-byte count
-                            } else {
-                                sent = true;
-                                ring = ring_put(ring, tl, t, c);
-                                mycells[ri] = ring.lo;
-                                mycells[ri + 64] = ring.hi;
-                                // the first broadcast of (node, type, key) is a SEND event, every later copy a COPY
-                                log_ev((wv & bit) ? BRC_EV_COPY : BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
-                                wv = ((wv | bit) & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                                mycells[(size_t)k * (CW * 64)] = wv;
-                                st_msgs += n;
-                            }
-                        } else if (!(wv & bit)) {
-                            sent = true;
-                            wv |= bit;
-                            wv = (wv & ~(0xFFFFull << sh)) | ((uint64_t)t << sh);
-                            mycells[(size_t)k * (CW * 64)] = wv;
-                            st_msgs += n;
-                            log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
+                if constexpr (!LEAN) {
+                    // a run of MSG records at this step (within the staged window): every lane applies
+                    // its own records at once, so their cell loads overlap (cfg3's equivocation pattern
+                    // is 80 such records per wave at step 1); then the wave-level effects in list order
+                    const uint32_t p0 = inj_pos - 1;
+                    uint32_t p1 = inj_pos;
+                    while (p1 < inj_cnt && p1 - injc_base < INJ_CACHE) {
+                        const InjDev q = inj_at(p1);
+                        if (q.t != t || q.kind != BRC_INJ_MSG) break;
+                        ++p1;
+                    }
+                    inj_pos = p1;
+                    uint32_t myrecs = 0, sentbits = 0;
+                    for (uint32_t p = p0; p < p1; ++p) {
+                        const InjDev q = inj_at(p);
+                        const bool mq = running && seg == (int)q.seg;
+                        mine_any |= mq;
+                        if (mq && d == q.node) myrecs |= 1u << (p - p0);
+                    }
+                    while (__any(myrecs != 0)) {
+                        if (myrecs) {
+                            const uint32_t i = (uint32_t)__ffs(myrecs) - 1u;
+                            myrecs &= myrecs - 1;
+                            if (msg_cell(inj_at(p0 + i))) sentbits |= 1u << i;
                         }
                     }
-                }
-                const uint32_t os = wave_or(sent ? outset : 0u);
-                if (os) {
-                    if (lane == 0) mark_lane(k, os, r.type);
-                    const uint32_t myq = seg_max<NPAD>(sent ? t + maxout : 0u);
-                    if (mine && myq) {
-                        if (d == 0) {
-                            const uint64_t m = s_meta[mbase + k];
-                            if (myq > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, myq);
-                        }
-                        q_until = max(q_until, myq);
+                    for (uint32_t p = p0; p < p1; ++p) {
+                        const InjDev q = inj_at(p);
+                        msg_marks(q, running && seg == (int)q.seg, ((sentbits >> (p - p0)) & 1u) != 0);
                     }
+                } else {
+                    msg_marks(r, mine, (mine && d == r.node) ? msg_cell(r) : false);
                 }
             }
             flush_clears();                          // PROPOSE / DELIVER may have started a key
@@ -858,7 +900,7 @@ void brc_step(const Params* __restrict__ pp) {
     }
 
 #ifdef BRC_STAMPS
-    uint64_t stamp_acc[4] = {0, 0, 0, 0};
+    uint64_t stamp_acc[5] = {0, 0, 0, 0, 0};
     uint32_t kcount[4] = {0, 0, 0, 0};
     uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
 #define BRC_STAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
@@ -1502,6 +1544,7 @@ void brc_step(const Params* __restrict__ pp) {
         any_rows |= uni32(wave_or(lane_rows));
         lane_rows = 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(3);
 
         // ================= per-instance stop conditions
         q_until = seg_max<NPAD>(q_until);
@@ -1531,12 +1574,12 @@ void brc_step(const Params* __restrict__ pp) {
             for (int c = 0; c < CHUNK; ++c) asm volatile("" ::"v"(w[c]));
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        BRC_STAMP(3);
+        BRC_STAMP(4);
     }
 
 #ifdef BRC_STAMPS
-    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
-    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[4 + i], (unsigned long long)kcount[i]);
+    if (lane == 0) for (int i = 0; i < 5; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[5 + i], (unsigned long long)kcount[i]);
 #endif
 #undef BRC_STAMP
     // ---- write back

@@ -173,13 +173,17 @@ class Engine:
             self._chk(self._lib.brc_read_events_range(self._h, first, arr, cap, ctypes.byref(total)))
         return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b, e.value) for e in arr[:cap]], total.value
 
-    def decisions(self):
-        """First decisions of the honest replicas: ({"-1": c, "0": c, "1": c, "3": c, "undecided": c},
-        instances whose honest replicas decided different values)."""
+    def decisions(self, labels=("-1", "0", "1", "3")):
+        """First decisions of the honest replicas: ({label of value id 0..3: c, "undecided": c},
+        instances whose honest replicas decided different values).  The default labels are the
+        wire codec's value table (Philox proposals); pass the strings your value ids stand for
+        (e.g. a Cluster's value table) to label loaded proposals."""
+        if len(labels) != 4 or len(set(labels)) != 4 or "undecided" in labels:
+            raise ValueError("labels: four distinct value strings, not 'undecided'")
         arr = np.zeros(5, dtype=np.uint64)
         dis = ctypes.c_uint64(0)
         self._chk(self._lib.brc_read_decisions(self._h, arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(dis)))
-        return dict(zip(("-1", "0", "1", "3", "undecided"), (int(x) for x in arr))), dis.value
+        return dict(zip(tuple(labels) + ("undecided",), (int(x) for x in arr))), dis.value
 
     def round_histogram(self, bins=66):
         """hist[r] = instances whose honest replicas had all decided by round r; hist[0] =

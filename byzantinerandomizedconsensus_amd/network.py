@@ -29,6 +29,11 @@ Deviations from the reference, all reported by exceptions and never silent:
   the wire, which its handler then ignores): other types raise ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
   (crashed) replicas.
+* A direct ``deliver()`` call (``core/byzantinerandomizedconsensus.py:53-60``) must carry a
+  string ``"message"`` from a ``"host"`` in the peer list.  The reference keys its value table
+  by the raw JSON value (so ``0`` and ``"0"`` are two values there) and adds an unknown host as
+  one more origin; the engine's value ids and origin bits cover neither, so both raise
+  ``EngineError``.
 
 Peers are identified as the shipped reference identifies them: by connection
 (``core/brbroadcast.py:69``; ``configure(peer_mode="sender")`` selects the commented-out :71
@@ -246,6 +251,12 @@ class Cluster:
         """ByzantineRandomizedConsensus.deliver called directly on replica i with a message of
         `host` (a peer address) carrying `message` (core/byzantinerandomizedconsensus.py:53-106):
         the replica's consensus state takes it at the current step, without BRB traffic."""
+        if not isinstance(message, str):
+            raise L.EngineError(L.E_UNSUPPORTED, "deliver(): message %r is not a string (the engine "
+                                "keys values by their string)" % (message,))
+        if not isinstance(message, str):
+            raise L.EngineError(L.E_UNSUPPORTED, "deliver(): message %r is not a string (the engine "
+                                "keys values by their string)" % (message,))
         h = _addr(host)
         if h not in self.index:
             raise L.EngineError(L.E_UNSUPPORTED, "deliver(): host %r is not in the peer list" % (h,))

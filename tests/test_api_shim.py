@@ -144,6 +144,9 @@ def test_direct_deliver_becomes_an_injection():
         [(L.INJ_DELIVER, 2, 4, "1")]
     with pytest.raises(L.EngineError):
         nodes[2].deliver(json.dumps(dict(msg, host=["elsewhere", 1])))
+    with pytest.raises(L.EngineError):                   # the reference keys 1 and "1" apart
+        nodes[2].deliver(json.dumps(dict(msg, message=1)))
+    assert len(c.actions) == 1
 
 
 def test_value_table_limits():

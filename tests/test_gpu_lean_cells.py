@@ -1,7 +1,7 @@
 """Edge cases of the lean kernels' compact cells (NPAD = 64, sender peers; brc_internal.h C32_*):
-send steps stored as 7-bit offsets from a per-item epoch that moves past step 100, slot
-generations kept mod 8 with the row rewritten fresh when a slot's tag wraps, and set sizes that
-saturate at 63.  Every case is checked bit-exact against the C oracle (or against the engine's own
+send steps stored as 7-bit offsets from a per-item epoch that moves past step 100, no slot
+generations (a slot's 64-cell row is rewritten fresh at every allocation: PROPOSE, a consensus
+SEND, an injected SEND / KEY), and set sizes that saturate at 63.  Every case is checked bit-exact against the C oracle (or against the engine's own
 first pass for repeated resets, whose first pass the oracle pins)."""
 import pytest
 
@@ -31,9 +31,10 @@ def _check(got, specs):
 
 
 @pytest.mark.parametrize("model,dmax,rcap", [(1, 5, 8), (3, 6, 14)])
-def test_spec_coin_rounds_wrap_tags_and_epochs(runner, model, dmax, rcap):
+def test_spec_coin_rounds_reallocate_rows_and_move_epochs(runner, model, dmax, rcap):
     """SPEC (common coin) at n = 64 with Q = 2: each round reallocates both slots of an origin
-    (the tag wraps at round 8) and the runs pass step 190 (the epoch moves twice)."""
+    (every allocation rewrites the slot's row, so no stale cell of the previous round may
+    survive it) and the runs pass step 190 (the epoch moves twice)."""
     specs = []
     for g in range(2):
         sp = S.spec_cons_spec(64, 21, 0x5EC64, model, dmax, 700 + g, round_cap=rcap, window=2, coin_seed=0xC0C0)
@@ -73,10 +74,10 @@ def test_epoch_moves_under_open_cells(runner):
     assert all(r["t_stop"] > 900 for r in got)
 
 
-def test_repeated_resets_wrap_slot_tags():
-    """Ten reset + run passes over one engine (cfg4 shape, 8 instances): every slot is
-    reallocated once per pass, so its 3-bit tag wraps and the row is rewritten fresh; each
-    pass must equal the first, which the oracle pins."""
+def test_repeated_resets_rewrite_rows():
+    """Ten reset + run passes over one engine (cfg4 shape, 8 instances): brc_reset leaves the
+    previous pass's cells in place and every slot is reallocated (its row rewritten fresh) in
+    each pass; each pass must equal the first, which the oracle pins."""
     from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd.engine import Engine
     specs = [S.cons_spec(64, 21, 0x5EED0004, 2, 8, 5000 + g, round_cap=1) for g in range(8)]

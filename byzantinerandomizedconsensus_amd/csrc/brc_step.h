@@ -853,7 +853,7 @@ void brc_step(const Params* __restrict__ pp) {
                 if constexpr (!LEAN) {
                     // a run of MSG records at this step (within the staged window): every lane applies
                     // its own records at once, so their cell loads overlap (cfg3's equivocation pattern
-                    // is 80 such records per wave at step 1); then the wave-level effects in list order
+                    // is 80 such records per wave at step 1)
                     const uint32_t p0 = inj_pos - 1;
                     uint32_t p1 = inj_pos;
                     while (p1 < inj_cnt && p1 - injc_base < INJ_CACHE) {
@@ -862,23 +862,34 @@ void brc_step(const Params* __restrict__ pp) {
                         ++p1;
                     }
                     inj_pos = p1;
-                    uint32_t myrecs = 0, sentbits = 0;
+                    uint32_t myrecs = 0;
                     for (uint32_t p = p0; p < p1; ++p) {
                         const InjDev q = inj_at(p);
                         const bool mq = running && seg == (int)q.seg;
                         mine_any |= mq;
                         if (mq && d == q.node) myrecs |= 1u << (p - p0);
                     }
+                    // the wave-level effects of a record reduce to its one sending lane: ring marks
+                    // at t + its link delays, its q_until, and the key's t_quiet (an LDS CAS: lanes
+                    // of other records may raise the same key's t_quiet)
                     while (__any(myrecs != 0)) {
                         if (myrecs) {
                             const uint32_t i = (uint32_t)__ffs(myrecs) - 1u;
                             myrecs &= myrecs - 1;
-                            if (msg_cell(inj_at(p0 + i))) sentbits |= 1u << i;
+                            const InjDev q = inj_at(p0 + i);
+                            if (msg_cell(q) && outset) {
+                                mark_lane(q.slot, outset, q.type);
+                                const uint32_t myq = t + maxout;
+                                q_until = max(q_until, myq);
+                                unsigned long long* mp = (unsigned long long*)&s_meta[mbase + q.slot];
+                                unsigned long long cur = *mp;
+                                while (m_tquiet(cur) < myq) {
+                                    const unsigned long long prev = atomicCAS(mp, cur, (unsigned long long)m_with_tquiet(cur, myq));
+                                    if (prev == cur) break;
+                                    cur = prev;
+                                }
+                            }
                         }
-                    }
-                    for (uint32_t p = p0; p < p1; ++p) {
-                        const InjDev q = inj_at(p);
-                        msg_marks(q, running && seg == (int)q.seg, ((sentbits >> (p - p0)) & 1u) != 0);
                     }
                 } else {
                     msg_marks(r, mine, (mine && d == r.node) ? msg_cell(r) : false);

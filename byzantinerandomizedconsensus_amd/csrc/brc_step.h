@@ -270,6 +270,12 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
     return r;
 }
 
+#ifndef BRC_NL_MSTORE
+#define BRC_NL_MSTORE 1      // non-lean kernels: exec-masked cell stores (0: whole-wave stores)
+#endif
+#ifndef BRC_LPK
+#define BRC_LPK 1            // non-lean kernels: narrow delay masks packed in a register (0: read from LDS)
+#endif
 #ifndef BRC_MIN_WAVES
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
@@ -466,6 +472,10 @@ void brc_step(const Params* __restrict__ pp) {
     // NLR: the (at most two) delays present -> registers: RL0/RL1 = masks, dly0/dly1 = delays,
     // OV0/OV1 = the wave's senders with such a link (wave-uniform)
     T RL0 = 0, RL1 = 0;
+    // LPK (narrow masks, few delays: NPAD = 16 at D <= 4, NPAD <= 8 at D <= 8): every compact mask
+    // packed into one u64 register, read by a shift instead of an LDS round trip per key
+    constexpr bool LPK = NLR == 0 && BRC_LPK && sizeof(T) * DM <= 8;
+    uint64_t Lpk = 0;
     uint32_t dly0 = 0, dly1 = 0;
     uint64_t OV0 = 0, OV1 = 0;
     if constexpr (NLR != 0) {
@@ -483,7 +493,11 @@ void brc_step(const Params* __restrict__ pp) {
         uint32_t j = 0;
 #pragma unroll
         for (int i = 0; i < DM; ++i)
-            if ((dset >> i) & 1) { if (j < nL) s_L[j * 64 + lane] = L[i]; ++j; }
+            if ((dset >> i) & 1) {
+                if (j < nL) s_L[j * 64 + lane] = L[i];
+                if constexpr (LPK) Lpk |= (uint64_t)L[i] << ((j * 8 * sizeof(T)) & 63);
+                ++j;
+            }
         if (j > nL) ovf = true;                      // cannot happen: delay_values() bounds dset
     }
     // lean ring marks (process_pair): lane L < 8 marks for delay class L & 1
@@ -491,6 +505,7 @@ void brc_step(const Params* __restrict__ pp) {
     // the j-th delay mask present in the wave (j < ndl)
     auto Lmask = [&](uint32_t j) -> T {
         if constexpr (NLR != 0) return j == 0 ? RL0 : RL1;
+        else if constexpr (LPK) return (T)(Lpk >> ((j * 8 * sizeof(T)) & 63));
         else return s_L[j * 64 + lane];
     };
     // cell (k, lane) at [k * CW * 64] (CONN send rings: ECHO at + 64, + 128, READY at + 192, + 256)
@@ -1304,11 +1319,15 @@ void brc_step(const Params* __restrict__ pp) {
             } else if constexpr (BEB) brb_cell_update_beb(fl, s_arr, es, rs, dl);
             else if constexpr (SPEC) brb_cell_update_spec(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
             else brb_cell_update(fl, ec, rc, s_arr, has ? ea : 0u, has ? ra : 0u, T_echo, T_amp, T_del, es, rs, dl);
-            {   // whole-wave store (lanes without arrivals write their word back unchanged)
+            {
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)ec << 5) | ((uint64_t)rc << 12) |
                                     ((uint64_t)gen << 19) | ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
-                mycells[(size_t)k * (CW * 64)] = has ? nw : wd;
+#if BRC_NL_MSTORE
+                if (has) mycells[(size_t)k * (CW * 64)] = nw;   // only cells with arrivals change
+#else
+                mycells[(size_t)k * (CW * 64)] = has ? nw : wd;  // whole-wave store (unchanged words back)
+#endif
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;

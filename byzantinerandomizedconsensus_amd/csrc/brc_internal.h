@@ -30,7 +30,10 @@ __host__ __device__ inline uint32_t gen32(uint16_t g) {
 __host__ __device__ constexpr uint32_t ring_steps(int dm) { return dm <= 8 ? 16u : 32u; }
 constexpr uint32_t STEP_LIMIT = 60000;
 constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before tags can wrap
-constexpr int CHUNK_W = 4;                  // wide kernel: keys whose ballots are exchanged per barrier
+#ifndef BRC_CHUNK_W
+#define BRC_CHUNK_W 4
+#endif
+constexpr int CHUNK_W = BRC_CHUNK_W;                // wide kernel: keys whose ballots are exchanged per barrier
 #ifndef BRC_WIDE_DCW
 #define BRC_WIDE_DCW 4
 #endif

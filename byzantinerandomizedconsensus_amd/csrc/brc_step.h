@@ -282,6 +282,32 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #ifndef BRC_MIN_WAVES_LEAN
 #define BRC_MIN_WAVES_LEAN 5 // ... for the one-instance-per-wave (lean) instantiations
 #endif
+#ifndef BRC_SPEC_MULTI
+#define BRC_SPEC_MULTI 0     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
+#endif
+#ifndef BRC_PK
+#define BRC_PK 0             // lean kernels: a key pair's cell updates in the two 16-bit halves of a register,
+                     // key metadata read only for pairs that use it
+#endif
+
+// Two u16 lanes per register (v_pk_*_u16): the lean kernels update the cells of a key PAIR with one
+// instruction per operation.  Every operand stays below 2^15 (set sizes <= 127, thresholds <= 65),
+// so pk_ge's sign test is exact in each half; results are 0/1 in bits 0 and 16.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pk_ge(uint32_t a, uint32_t b) { return (~pk_sub(a, b) >> 15) & 0x10001u; }
+__device__ __forceinline__ uint32_t pk2(uint32_t x) { return x | (x << 16); }   // x < 2^16 in both halves
 
 // Lean instantiations: one instance per wave (NPAD = 64, IPW = 1) with sender-identity peers.
 // Every key-slot field is then wave-uniform, so the per-key work runs on scalar key ids,
@@ -1058,7 +1084,8 @@ void brc_step(const Params* __restrict__ pp) {
                     if (tb[i] & TB_S) {
                         // SEND from the key's origin: lands on d iff delay(origin -> d) == t - t_send, and
                         // the key list holds the key now only for such a delay of the origin's outset
-                        const uint32_t dt = t - m_tsend(m[i]), snd = m_sender(m[i]);
+                        const uint64_t mi = uni64(m[i]);                 // the row is wave-uniform
+                        const uint32_t dt = t - m_tsend(mi), snd = m_sender(mi);
                         bool hit;
                         if constexpr (NLR != 0) {
                             hit = (((RL0 >> snd) & 1) != 0) == (dt == dly0);
@@ -1067,7 +1094,7 @@ void brc_step(const Params* __restrict__ pp) {
                             hit = (s_L[sj * 64 + lane] >> snd) & 1;
                         }
                         uint64_t hm = __ballot(hit) & hon_mask;
-                        if (m[i] & M_RESTRICTED) hm &= __ballot((gp(P.kdst)[inst * NK + k[i]] >> d) & 1ull);
+                        if (mi & M_RESTRICTED) hm &= __ballot((gp(P.kdst)[inst * NK + k[i]] >> d) & 1ull);
                         sa[i] = lane_in(hm) ? 1u : 0u;
                     }
                 }
@@ -1096,7 +1123,65 @@ void brc_step(const Params* __restrict__ pp) {
                 opn[i] = lane_in(ob[i]);
                 fl[i] = lo[i] & 31u; ec[i] = (lo[i] >> C32_EC_SH) & 63u; rc[i] = (lo[i] >> C32_RC_SH) & 63u;
             }
-            if constexpr (BEB) {
+            constexpr bool PK = BRC_PK && !BEB;
+            uint32_t FL = 0, EC = 0, RC = 0;     // PK: key 0 in bits 0-15, key 1 in bits 16-31
+            if constexpr (PK) {
+                // the same transitions as the per-key code below (brb_cell_update / _spec), both keys at once
+                const uint32_t P0 = (lo[0] & 0xFFFFu) | (lo[1] << 16);              // flags + |E|
+                const uint32_t P1 = ((lo[0] >> 8) & 0xFFFFu) | ((lo[1] >> 8) << 16); // |R| at bits 3-8
+                FL = P0 & 0x001F001Fu;
+                EC = (P0 >> C32_EC_SH) & 0x003F003Fu;
+                RC = (P1 >> (C32_RC_SH - 8)) & 0x003F003Fu;
+                const uint32_t ONM = (opn[0] ? 0xFFFFu : 0u) | (opn[1] ? 0xFFFF0000u : 0u), ON = ONM & 0x10001u;
+                const uint32_t SA = (sa[0] | (sa[1] << 16)) & ONM;
+                const uint32_t E = (ea[0] | (ea[1] << 16)) & ONM, R = (ra[0] | (ra[1] << 16)) & ONM;
+                // x != 0 per half for halves <= 128 (min(x, 1) is split per half by the compiler)
+                auto nz = [](uint32_t x) -> uint32_t { return ((x + 0x007F007Fu) >> 7) & 0x10001u; };
+                uint32_t ES = 0, RS = 0, DL = 0;
+                if constexpr (SPEC) {
+                    if (tbu & TB_S) { ES = SA & ~(FL >> 3) & 0x10001u; FL |= ES << 3; }        // !F_ES
+                    if (tbu & (TB_E | TB_R)) {
+                        EC = pk_add(EC, E);
+                        RC = pk_add(RC, R);
+                        RS = ON & ~(FL >> 4) & (pk_ge(EC, pk2(T_echo)) | pk_ge(RC, pk2(T_amp)));  // !F_RS
+                        FL |= RS << 4;
+                        DL = ON & pk_ge(RC, pk2(T_del));
+                        FL |= DL << 2;
+                    }
+                } else {
+                    if (tbu & TB_S) {                                                   // :76-82
+                        const uint32_t est = SA & ~FL & 0x10001u;                       // SEND, no ECHO entry
+                        ES = est & ~(FL >> 3);                                          // not sent already
+                        FL |= est | (est << 3);                                         // F_EEX | F_ES
+                    }
+                    if (tbu & TB_E) {                                                   // :84-98
+                        const uint32_t eon = nz(E);
+                        const uint32_t chk = nz(E + (FL & 0x10001u) - eon);             // a checked ECHO (:87-89)
+                        FL |= eon;
+                        EC = pk_add(EC, E);
+                        const uint32_t r1 = eon & chk & pk_ge(EC, pk2(T_echo)) & (~FL >> 1) & 0x10001u;  // !F_REX (:95)
+                        RS = r1 & ~(FL >> 4);
+                        FL |= (r1 << 1) | (r1 << 4);
+                    }
+                    if (tbu & TB_R) {                                                   // :100-119
+                        const uint32_t ron = nz(R);
+                        const uint32_t rexm = pk_sub(0u, (FL >> 1) & 0x10001u);        // 0xFFFF per half iff F_REX
+                        const uint32_t rlo = pk_add(pk_sub(RC, 0x10001u) & rexm, 0x20002u), rhi = pk_add(R, RC & rexm);
+                        FL |= ron << 1;
+                        RC = pk_add(RC, R);
+                        const uint32_t any = ron & pk_ge(rhi, rlo);
+                        const uint32_t alo = pk_max(rlo, pk2(T_amp)), ahi = pk_min(rhi, pk2(T_del - 1u));
+                        const uint32_t r2 = any & ~FL & ~(FL >> 4) & pk_ge(ahi, alo) & 0x10001u;   // !F_EEX, !F_RS
+                        FL |= r2 << 4;
+                        DL = any & pk_ge(rhi, pk2(T_del));
+                        FL |= DL << 2;
+                        RS |= r2;
+                    }
+                }
+                es[0] = ES & 1u; es[1] = ES >> 16;
+                rs[0] = RS & 1u; rs[1] = RS >> 16;
+                dl[0] = DL & 1u; dl[1] = DL >> 16;
+            } else if constexpr (BEB) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     dl[i] = (opn[i] && sa[i]) ? 1u : 0u;         // brb_cell_update_beb
@@ -1166,13 +1251,18 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
             uint64_t eb[2], rb[2], db[2];
+            // PK: flags and |E| of both keys, |R| apart (its field crosses bit 16)
+            const uint32_t PL = FL | (pk_min(EC, 0x003F003Fu) << C32_EC_SH), PR = pk_min(RC, 0x003F003Fu);
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 // new word for open cells; the others keep theirs.  A count reaches 64 only when every
                 // sender's message of that type has arrived, so none is compared again: the stored
                 // counts saturate at 63 without changing any later transition
-                nw[i] = fl[i] | (min(ec[i], 63u) << C32_EC_SH) | (min(rc[i], 63u) << C32_RC_SH) |
-                        ((es[i] ? ts : tE[i]) << C32_OE_SH) | ((rs[i] ? ts : tR[i]) << C32_OR_SH);
+                const uint32_t sends = ((es[i] ? ts : tE[i]) << C32_OE_SH) | ((rs[i] ? ts : tR[i]) << C32_OR_SH);
+                if constexpr (PK)
+                    nw[i] = ((PL >> (16 * i)) & 0xFFFFu) | (((PR >> (16 * i)) & 0xFFFFu) << C32_RC_SH) | sends;
+                else
+                    nw[i] = fl[i] | (min(ec[i], 63u) << C32_EC_SH) | (min(rc[i], 63u) << C32_RC_SH) | sends;
                 wr[i] = opn[i];
                 eb[i] = __ballot(es[i] != 0); rb[i] = __ballot(rs[i] != 0); db[i] = __ballot(dl[i] != 0);
             }
@@ -1199,10 +1289,11 @@ void brc_step(const Params* __restrict__ pp) {
             if (EV) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const uint32_t kp = (k[i] >> qsh), s = m_s1(m[i]) - 1u;
-                    if (es[i]) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m[i]));
-                    if (rs[i]) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(m[i]));
-                    if (dl[i]) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m[i]));
+                    const uint64_t mi = uni64(m[i]);
+                    const uint32_t kp = (k[i] >> qsh), s = m_s1(mi) - 1u;
+                    if (es[i]) log_ev(BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(mi));
+                    if (rs[i]) log_ev(BRC_EV_SEND, d, BRC_READY, kp, s, m_value(mi));
+                    if (dl[i]) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(mi));
                 }
             }
             // sends: typed ring marks at t + every delay some sending lane has (the step's ring rows,
@@ -1394,7 +1485,8 @@ void brc_step(const Params* __restrict__ pp) {
                 uint64_t mm[CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    mm[c] = s_meta[kk[c] & TB_KEY];
+                    // the metadata is read only where the pair uses it: SEND arrivals and the event log
+                    mm[c] = (EV || !BRC_PK || ((kk[c] >> TB_SH) & TB_S)) ? s_meta[kk[c] & TB_KEY] : 0ull;
                 });
                 // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
                 // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own
@@ -1405,7 +1497,7 @@ void brc_step(const Params* __restrict__ pp) {
                     // a pair past the list is skipped; the second key of a pair at the list's end is
                     // the padding entry (the trash row, no message type): it changes nothing
                     const uint32_t ent[2] = {kk[c], kk[c + 1]};
-                    const uint64_t mp[2] = {uni64(mm[c]), uni64(mm[c + 1])};
+                    const uint64_t mp[2] = {mm[c], mm[c + 1]};
                     const uint32_t lo[2] = {w[c], w[c + 1]};
                     uint32_t nw[2] = {w[c], w[c + 1]};
                     bool wr[2] = {false, false};
@@ -1483,16 +1575,23 @@ void brc_step(const Params* __restrict__ pp) {
                     const uint64_t hb = __ballot(bits != 0);
                     if (!seen_on && hb) {
                         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
-                        const uint32_t c0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)hb) - 1));
-                        if (!__ballot(bits != 0 && cur != c0)) {
-                            const uint32_t sn = s_snap[w * 64 + lane];
-                            const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;   // slot w*64+lane
+                        const uint32_t sn = s_snap[w * 64 + lane];
+                        const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;   // slot w*64+lane
+                        const uint64_t v1 = __ballot(sv == 1), v2 = __ballot(sv == 2);
+                        // one pass per distinct phase index c0 among the delivering lanes (one, or two at a
+                        // phase boundary; BRC_SPEC_MULTI = 0: only words whose lanes share one index)
+                        uint64_t pend = hb;
+                        while (pend) {
+                            const uint32_t c0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)pend) - 1));
+                            const bool at = bits != 0 && cur == c0;
+                            const uint64_t bat = __ballot(at);
+                            if (!BRC_SPEC_MULTI && bat != pend) break;
+                            pend &= ~bat;
                             const uint64_t inw = __ballot(ss >= c0 && ss - c0 < Q), atc = __ballot(ss == c0);
                             const uint64_t past = __ballot(ss != 0xFFFFFFFFu && ss >= c0 && ss - c0 >= Q);
-                            const uint64_t v1 = __ballot(sv == 1), v2 = __ballot(sv == 2);
                             const uint32_t ncur = (uint32_t)__popcll(bits & atc);
                             const uint32_t qc = c0 & Qm;
-                            if (bits && (round == 0 || (s_cnt[qc * 64 + lane] & 0x3FFu) + ncur < n - P.f)) {
+                            if (at && (round == 0 || (s_cnt[qc * 64 + lane] & 0x3FFu) + ncur < n - P.f)) {
                                 if (bits & past) ovf = true;                  // beyond the window (spec_deliver)
                                 const uint64_t b = bits & inw;
                                 // slots of phase slot q (slot mod Q == q): bit q of every Q-bit group

@@ -283,11 +283,13 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #define BRC_MIN_WAVES_LEAN 5 // ... for the one-instance-per-wave (lean) instantiations
 #endif
 #ifndef BRC_SPEC_MULTI
-#define BRC_SPEC_MULTI 0     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
+#define BRC_SPEC_MULTI 1     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
 #endif
 #ifndef BRC_PK
-#define BRC_PK 0             // lean kernels: a key pair's cell updates in the two 16-bit halves of a register,
-                     // key metadata read only for pairs that use it
+#define BRC_PK 1             // lean kernels: a key pair's cell updates in the two 16-bit halves of a register
+#endif
+#ifndef BRC_LAZY_META
+#define BRC_LAZY_META 0      // lean kernels: key metadata read only for pairs with a SEND arrival (A/B: +1 %)
 #endif
 
 // Two u16 lanes per register (v_pk_*_u16): the lean kernels update the cells of a key PAIR with one
@@ -1485,8 +1487,8 @@ void brc_step(const Params* __restrict__ pp) {
                 uint64_t mm[CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    // the metadata is read only where the pair uses it: SEND arrivals and the event log
-                    mm[c] = (EV || !BRC_PK || ((kk[c] >> TB_SH) & TB_S)) ? s_meta[kk[c] & TB_KEY] : 0ull;
+                    // LAZY_META: the metadata is read only where the pair uses it (SEND arrivals, event log)
+                    mm[c] = (EV || !BRC_LAZY_META || ((kk[c] >> TB_SH) & TB_S)) ? s_meta[kk[c] & TB_KEY] : 0ull;
                 });
                 // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
                 // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own

@@ -48,13 +48,56 @@ template <> struct MaskOf<32> { using type = uint32_t; };
 
 template <typename T> __device__ __forceinline__ uint32_t popc(T x) { return (uint32_t)__popcll((uint64_t)x); }
 
+
+// Whole-wave reductions (NPAD = 64) through DPP row operations and four lane reads: each 16-lane
+// row reduces with quad_perm xor 1 and xor 2, row_half_mirror and row_mirror, and the four row
+// results combine in scalar registers -- no LDS round trip and no shuffle-address registers.  Every
+// lane must be active (the step loop's reductions run in wave-uniform control flow); otherwise the
+// shuffle form below is used.
+__device__ __forceinline__ uint32_t dpp_row_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);   // row_half_mirror
+    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);   // row_mirror
+    return x;
+}
+__device__ __forceinline__ uint32_t dpp_row_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true));
+    x = max(x, (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true));
+    return x;
+}
+__device__ __forceinline__ bool full_exec() { return __builtin_amdgcn_read_exec() == ~0ull; }
+__device__ __forceinline__ uint32_t rl(uint32_t x, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); }
+
+// OR / max over every lane, called with every lane active (wave-uniform control flow)
+__device__ __forceinline__ uint32_t wave_or_all(uint32_t x) {
+    const uint32_t r = dpp_row_or(x);
+    return rl(r, 0) | rl(r, 16) | rl(r, 32) | rl(r, 48);
+}
+__device__ __forceinline__ uint32_t wave_max_all(uint32_t x) {
+    const uint32_t r = dpp_row_max(x);
+    return max(max(rl(r, 0), rl(r, 16)), max(rl(r, 32), rl(r, 48)));
+}
+// OR of every lane's x (the same value in every lane)
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    if (full_exec()) {
+        const uint32_t r = dpp_row_or(x);
+        return rl(r, 0) | rl(r, 16) | rl(r, 32) | rl(r, 48);
+    }
 #pragma unroll
     for (int o = 32; o; o >>= 1) x |= (uint32_t)__shfl_xor((int)x, o);
     return x;
 }
 
 template <int NPAD> __device__ __forceinline__ uint32_t seg_max(uint32_t x) {
+    if constexpr (NPAD == 64) {
+        if (full_exec()) {
+            const uint32_t r = dpp_row_max(x);
+            return max(max(rl(r, 0), rl(r, 16)), max(rl(r, 32), rl(r, 48)));
+        }
+    }
 #pragma unroll
     for (int o = NPAD / 2; o; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
     return x;
@@ -451,9 +494,9 @@ void brc_step(const Params* __restrict__ pp) {
             for (int i = 0; i < DM; ++i) if ((uint32_t)i + 1 == P.dconst) L[i] = allm;
         } else if (P.delay_model == BRC_DELAY_SLOWSET) {
             const uint32_t off = slow_offset(P.seed, g, n);
-            T slowm = 0;
-            for (uint32_t j = 0; j < n; ++j) if (((j + n - off) % n) < P.f) slowm |= (T)((T)1 << j);
             const bool me_slow = ((uint32_t)d + n - off) % n < P.f;
+            // the slow set of this lane's instance: its segment's lanes with me_slow
+            const T slowm = (T)(__ballot(me_slow) >> segbase);
 #pragma unroll
             for (int i = 0; i < DM; ++i) {
                 if ((uint32_t)i + 1 == D) L[i] |= me_slow ? allm : slowm;
@@ -489,7 +532,7 @@ void brc_step(const Params* __restrict__ pp) {
         if (lane == i) outv = b;
     }
     const uint32_t maxout = hibit(outset);
-    const uint32_t dset = uni32(wave_or(outset));    // every delay some link of this wave has
+    const uint32_t dset = wave_or_all(outset);       // every delay some link of this wave has
     // dlist: the delays present, minus one, 4 bits each in ascending order; ndl of them
     uint64_t dlist = 0;
     uint32_t ndl = 0;
@@ -540,8 +583,16 @@ void brc_step(const Params* __restrict__ pp) {
     const gptr_t<uint64_t> mycells = gp(P.cells) + item * (uint64_t)(NK + 1) * CW * 64 + lane;
     // lean SPEC: this wave's HBM delivery-bitmap row, word w at [w * 64]
     const gptr_t<uint64_t> gdbits = gp(P.dbits) + item * (uint64_t)nkw * 64 + lane;
-    // lean kernels: compact u32 cells (brc_internal.h C32_*), row k at [k * 64]
-    const gptr_t<uint32_t> ccells = gp((uint32_t*)P.cells) + item * (uint64_t)(NK + 1) * 64;
+    // lean kernels: compact u32 cells (brc_internal.h C32_*), row k at [k * 64].  Accessed through a
+    // buffer resource over the item's rows (base and size in SGPRs): a row access is one
+    // buffer_load/store_dword with voffset = 4 lane (a constant VGPR) and soffset = 256 k (an SGPR),
+    // no per-lane 64-bit address arithmetic; a row index past the item's rows reads 0 and drops stores
+    const __amdgpu_buffer_rsrc_t crs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)((uint32_t*)P.cells + item * (uint64_t)(NK + 1) * 64), (short)0,
+                                          (int)((NK + 1) * 256u), 0x00020000);
+    const uint32_t lv4 = (uint32_t)lane * 4u;
+    auto cld = [&](uint32_t k) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(crs, lv4, k * 256u, 0); };
+    auto cst = [&](uint32_t k, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, crs, lv4, k * 256u, 0); };
     // lean: this lane's own key slots (bit s mod Q) allocated since the last flush; the wave
     // rewrites those rows fresh (flush_clears) before anything reads them
     uint32_t clr = 0;
@@ -551,7 +602,7 @@ void brc_step(const Params* __restrict__ pp) {
                 const int L = __ffsll((unsigned long long)b) - 1;
                 for (uint32_t cm = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr, L)); cm; cm &= cm - 1) {
                     const uint32_t k = ((uint32_t)L * NV) * Q + (uint32_t)__ffs(cm) - 1u;
-                    (ccells + (size_t)k * 64)[lane] = C32_FRESH;
+                    cst(k, C32_FRESH);
                 }
             }
             clr = 0;
@@ -565,12 +616,11 @@ void brc_step(const Params* __restrict__ pp) {
             const uint32_t nep = t - C32_KEEP, delta = nep - ep;
             for (uint32_t k = 0; k < NK; ++k) {
                 if (m_s1(uni64(s_meta[k])) == 0) continue;
-                const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
-                const uint32_t c = *p;
+                const uint32_t c = cld(k);
                 uint32_t oE = (c >> C32_OE_SH) & 127u, oR = c >> C32_OR_SH;
                 if (oE < C32_OLD) oE = oE >= delta ? oE - delta : C32_OLD;
                 if (oR < C32_OLD) oR = oR >= delta ? oR - delta : C32_OLD;
-                *p = (c & ((1u << C32_OE_SH) - 1u)) | (oE << C32_OE_SH) | (oR << C32_OR_SH);
+                cst(k, (c & ((1u << C32_OE_SH) - 1u)) | (oE << C32_OE_SH) | (oR << C32_OR_SH));
             }
             ep = nep;
         }
@@ -754,13 +804,12 @@ void brc_step(const Params* __restrict__ pp) {
             badinj = true;
         } else if constexpr (LEAN) {
             // compact cell: F_ES / F_RS and the send-step offset
-            const gptr_t<uint32_t> p = ccells + (size_t)k * 64 + lane;
-            const uint32_t wv = *p;
+            const uint32_t wv = cld(k);
             const uint32_t bit = (r.type == BRC_ECHO) ? F_ES : F_RS;
             const uint32_t sh = (r.type == BRC_ECHO) ? C32_OE_SH : C32_OR_SH;
             if (!(wv & bit)) {
                 sent = true;
-                *p = ((wv | bit) & ~(127u << sh)) | ((t - ep) << sh);
+                cst(k, ((wv | bit) & ~(127u << sh)) | ((t - ep) << sh));
                 st_msgs += n;
                 log_ev(BRC_EV_SEND, d, r.type, (k >> qsh), r.s, m_value(m));
             }
@@ -888,7 +937,7 @@ void brc_step(const Params* __restrict__ pp) {
                         }
                     }
                     if constexpr (LEAN) {
-                        if (__ballot(fresh)) (ccells + (size_t)k * 64)[lane] = C32_FRESH;
+                        if (__ballot(fresh)) cst(k, C32_FRESH);
                     }
                     q_until = max(q_until, t + hibit(os));
                 }
@@ -947,8 +996,8 @@ void brc_step(const Params* __restrict__ pp) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if (its.initialized == 0 && t == 0) {
         do_actions();
-        q_until = seg_max<NPAD>(q_until);
-        any_rows |= uni32(wave_or(lane_rows));
+        q_until = NPAD == 64 ? wave_max_all(q_until) : seg_max<NPAD>(q_until);
+        any_rows |= wave_or_all(lane_rows);
         lane_rows = 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
@@ -1002,9 +1051,17 @@ void brc_step(const Params* __restrict__ pp) {
                 // slot k lands now at some receiver iff t - t_send is a delay of its sender's outset
                 const uint64_t mE = uni64(s_act[(row * AT + 0) * nkw + w]), mR = uni64(s_act[(row * AT + 1) * nkw + w]);
                 const uint64_t m = s_meta[w * 64 + lane];
-                const uint32_t dt1 = t - m_tsend(m) - 1u;                  // delay - 1 of a SEND landing now
-                const uint32_t os = (uint32_t)__shfl((int)outset, (int)m_sender(m));
-                const bool sl = m_s1(m) != 0 && dt1 < 32u && ((os >> (dt1 & 31u)) & 1u);
+                const uint32_t dt = t - m_tsend(m);                        // the delay of a SEND landing now
+                bool sl;
+                if constexpr (NLR != 0) {
+                    // OV0 / OV1: the senders with a link of delay dly0 / dly1 to an honest receiver
+                    const uint32_t snd = m_sender(m) & 63u;
+                    sl = m_s1(m) != 0 && ((dt == dly0 && ((OV0 >> snd) & 1ull)) || (dt == dly1 && ((OV1 >> snd) & 1ull)));
+                } else {
+                    const uint32_t dt1 = dt - 1u;
+                    const uint32_t os = (uint32_t)__shfl((int)outset, (int)m_sender(m));
+                    sl = m_s1(m) != 0 && dt1 < 32u && ((os >> (dt1 & 31u)) & 1u);
+                }
                 tb = (sl ? TB_S : 0u) | ((uint32_t)(mE >> lane) & 1u) * TB_E | ((uint32_t)(mR >> lane) & 1u) * TB_R;
                 bits = __ballot(tb != 0);
             } else {
@@ -1474,7 +1531,7 @@ void brc_step(const Params* __restrict__ pp) {
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
-            auto cell = [&](uint32_t e) { return (ccells + (size_t)(e & TB_KEY) * 64)[lane]; };
+            auto cell = [&](uint32_t e) { return cld(e & TB_KEY); };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
             Unrolled<CHUNK>::run([&](auto ci) {
@@ -1504,8 +1561,8 @@ void brc_step(const Params* __restrict__ pp) {
                     uint32_t nw[2] = {w[c], w[c + 1]};
                     bool wr[2] = {false, false};
                     if (p + c < nkeys) process_pair(ent, mp, lo, nw, wr);
-                    if (wr[0]) (ccells + (size_t)(kk[c] & TB_KEY) * 64)[lane] = nw[0];
-                    if (wr[1]) (ccells + (size_t)(kk[c + 1] & TB_KEY) * 64)[lane] = nw[1];
+                    if (wr[0]) cst(kk[c] & TB_KEY, nw[0]);
+                    if (wr[1]) cst(kk[c + 1] & TB_KEY, nw[1]);
                     kk[c] = (uint32_t)(uni64(knext) >> (16 * c)) & 0xFFFFu;
                     w[c] = cell(kk[c]);
                     kk[c + 1] = (uint32_t)(uni64(knext) >> (16 * (c + 1))) & 0xFFFFu;
@@ -1539,7 +1596,7 @@ void brc_step(const Params* __restrict__ pp) {
             uint32_t rb = 0;
             for (uint32_t i = lane; i < RS * AT * nkw; i += 64)
                 if (s_act[i] != 0) rb |= 1u << (i >> rsh);
-            rb = uni32(wave_or(rb)) & ~(1u << row);
+            rb = wave_or_all(rb) & ~(1u << row);
             if (rb) {
                 any_rows |= rb;
                 const uint32_t rel = (row ? ((rb >> row) | (rb << (RS - row))) : rb) & (RS == 32 ? ~0u : ((1u << RS) - 1u));
@@ -1672,13 +1729,13 @@ void brc_step(const Params* __restrict__ pp) {
 
         // ================= actions stamped t
         const bool inj_mine = do_actions();
-        any_rows |= uni32(wave_or(lane_rows));
+        any_rows |= wave_or_all(lane_rows);
         lane_rows = 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(3);
 
         // ================= per-instance stop conditions
-        q_until = seg_max<NPAD>(q_until);
+        q_until = NPAD == 64 ? wave_max_all(q_until) : seg_max<NPAD>(q_until);
         const uint64_t b_act = __ballot(st_cells != cells0 || inj_mine) & segbits;
         const uint64_t b_ovf = __ballot(ovf) & segbits;
         const uint64_t b_bad = __ballot(badinj) & segbits;

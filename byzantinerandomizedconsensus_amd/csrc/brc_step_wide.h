@@ -289,6 +289,7 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
             }
         }
     };
+    bool fmark = false;          // this thread marked a slot row fresh since the last clear_fresh
     auto mark_lane = [&](uint32_t k, uint32_t ds) {
         while (ds) {
             const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
@@ -303,6 +304,7 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
         if ((m_s1(m) != 0 && t < m_tquiet(m)) || s >= P.s_limit) { ovf = true; return; }
         atomicOr((unsigned long long*)&s_fresh[k >> 6], 1ull << (k & 63));   // the row is rewritten (clear_fresh)
+        fmark = true;
         s_meta[k] = m_pack(s + 1, t, t + maxout, d, v);
         mark_lane(k, outset);
         q_until = max(q_until, t + maxout);
@@ -330,8 +332,11 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
     };
     // rewrite the rows of the slots allocated since the last call to "never sent" (each thread its
     // own cell; the connection-peer send rings are ignored while the cell reads never sent)
+    // One barrier (with the "any thread marked a row" vote) when no slot was allocated since the
+    // last call: injection records that allocate nothing pay no row sweep.
     auto clear_fresh = [&]() {
-        __syncthreads();
+        if (!__syncthreads_or(fmark ? 1 : 0)) return;
+        fmark = false;
         for (uint32_t w = 0; w < nkw; ++w)
             for (uint64_t x = s_fresh[w]; x; x &= x - 1)
                 mycells[(size_t)(w * 64 + (uint32_t)__builtin_ctzll(x)) * (CW * NPAD)] = TIMES_NEVER;
@@ -470,7 +475,7 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
                             ovf = true;
                         } else {
                             uint32_t tq = m_tquiet(m);
-                            if (!declared) { tq = t + 1; s_fresh[k >> 6] |= 1ull << (k & 63); }
+                            if (!declared) { tq = t + 1; s_fresh[k >> 6] |= 1ull << (k & 63); fmark = true; }
                             if (is_send) tq = max(tq, t + hibit(os));
                             m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
                             s_meta[k] = m | (restricted ? M_RESTRICTED : 0ull);

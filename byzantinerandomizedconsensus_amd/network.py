@@ -254,9 +254,6 @@ class Cluster:
         if not isinstance(message, str):
             raise L.EngineError(L.E_UNSUPPORTED, "deliver(): message %r is not a string (the engine "
                                 "keys values by their string)" % (message,))
-        if not isinstance(message, str):
-            raise L.EngineError(L.E_UNSUPPORTED, "deliver(): message %r is not a string (the engine "
-                                "keys values by their string)" % (message,))
         h = _addr(host)
         if h not in self.index:
             raise L.EngineError(L.E_UNSUPPORTED, "deliver(): host %r is not in the peer list" % (h,))

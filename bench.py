@@ -103,11 +103,12 @@ def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
                       % (count, count - 1, dt, threads, arrivals / dt)}
 
 
-def load_traffic(instances, kernel_ms, mode="reference"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/pmc_traffic.json for
-    the reference leg, profiles/pmc_traffic_<mode>.json for the others, written by
-    profiles/summarize.py), used only if it was taken on this workload and size and its kernel time
-    agrees with the live one within 15 % (i.e. the same kernel build)."""
+def load_profile(instances, kernel_ms, mode="reference"):
+    """The committed rocprofv3 summary of this leg (profiles/pmc_traffic.json for the reference leg,
+    profiles/pmc_traffic_<mode>.json for the others, written by profiles/summarize.py): HBM bytes per
+    launch and the instruction-issue block.  Used only if it was taken on this workload and size and
+    its kernel time agrees with the live one within 15 % (the same kernel build); the agreement is
+    reported beside it."""
     name = "pmc_traffic.json" if mode == "reference" else "pmc_traffic_%s.json" % mode
     path = os.path.join(ROOT, "profiles", name)
     try:
@@ -120,7 +121,7 @@ def load_traffic(instances, kernel_ms, mode="reference"):
         return None
     if abs(d["avg_ns"] / 1e6 - kernel_ms) > 0.15 * kernel_ms:
         return None
-    return d.get("hbm_bytes_per_launch")
+    return d
 
 
 def make_engine(mode, count, first, device, round_cap):
@@ -212,15 +213,18 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     launches = len(tiles)
     cs_gpu = cell_steps / world
     secs = kernel_ms / 1e3
-    traffic = load_traffic(per, kernel_ms, mode) if launches == 1 else None
-    if kernel != "step":
+    prof = load_profile(per, kernel_ms, mode) if launches == 1 else None
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
+    if kernel not in ("step", "life"):
+        raise SystemExit("%s leg: the launches ran different kernels (%s); its roofline cannot be priced" % (mode, kernel))
+    if kernel == "life":
         # the key-lifetime kernel (csrc/brc_life.h) keeps a key's cells in registers for its whole
         # lifetime: no cell bytes move, HBM carries only the per-instance results
         roof = {"bound": "issue", "kernel": "brc_life", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": None, "traffic": traffic,
                 "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "survey_model_frac": SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9 / HBM_PEAK_GBS,
-                "cell_steps_per_s": cs_gpu / secs,
+                "cell_steps_per_s": cs_gpu / secs, "cell_bytes": 0,
                 "note": "no HBM cell traffic (cells stay in registers for a key's lifetime): bound by instruction "
                         "issue, not HBM; survey_model_frac prices SURVEY 8(d)'s %d B per cell-step"
                         % SURVEY_BYTES_PER_CELL_STEP}
@@ -239,6 +243,13 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
                         "credits n-bit ECHO/READY masks this design never moves, so it can pass 1"
                         % (FLOOR_BYTES_PER_CELL_STEP, CELL_BYTES, cs_gpu, launches, "" if launches == 1 else "es",
                            SURVEY_BYTES_PER_CELL_STEP)}
+    if prof:
+        # the same-build profile: its kernel time beside the live one, and its issue view (VALU busy,
+        # SALU per CU-cycle, wave-cycle split) -- these kernels are issue- and latency-bound
+        roof["profile"] = {"source": prof.get("source"), "kernel_ms": prof["avg_ns"] / 1e6,
+                           "agreement": prof["avg_ns"] / 1e6 / kernel_ms}
+        if prof.get("issue"):
+            roof["issue"] = prof["issue"]
     leg = {
         "value": decided * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -301,7 +312,10 @@ def main():
             "dtype": "u32",
             "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
             "config": {"workload": head["workload"], "n": N_REPLICAS, "f": F_FAULTS,
-                       "instances_per_gpu": args.instances, "round_cap": args.round_cap, "mode": head_mode,
+                       "instances_per_gpu": args.instances, "round_cap": args.round_cap,
+                       "round_cap_meaning": "an instance is done when every honest replica has decided this many "
+                                            "times (the run stops at that decision, not a give-up bound)",
+                       "mode": head_mode,
                        "key_window": 8 if head_mode == "spec" else 4,
                        "peer_mode": "connection" if head_mode == "conn" else "sender",
                        "parallelism": "instance-sharded x%d" % world},

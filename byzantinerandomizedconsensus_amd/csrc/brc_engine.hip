@@ -370,8 +370,10 @@ int brc_create(const brc_config* cfg, void** out) {
         (c.peer_mode == BRC_PEER_CONNECTION && c.mode != BRC_MODE_REFERENCE) ||
         (c.protocol != BRC_PROTO_BRB && c.protocol != BRC_PROTO_CONSENSUS) || c.delay_model > BRC_DELAY_GEOMETRIC ||
         (c.delay_model == BRC_DELAY_CONST && (c.delay_const < 1 || c.delay_const > c.delay_max)) ||
-        !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8) ||
-        !(c.variants == 1 || c.variants == 2 || c.variants == 4) || c.key_window * c.variants > 8 ||
+        !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8 || c.key_window == 16 || c.key_window == 32) ||
+        !(c.variants == 1 || c.variants == 2 || c.variants == 4) ||
+        // more than 8 live phase indices per origin: reference / best-effort protocols on the narrow kernels
+        c.key_window * c.variants > ((c.mode != BRC_MODE_SPEC && c.n <= 64) ? 32u : 8u) ||
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
         c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB ||
@@ -423,7 +425,9 @@ int brc_create(const brc_config* cfg, void** out) {
                               c.delay_max <= 8 && e->life_lds <= 64 * 1024;
         e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION);
     }
-    if (e->nkw > (uint32_t)e->nkw_t || e->nitems > 0x7FFFFFFFull * WPB || e->lds_bytes > 160 * 1024) {
+    // narrow kernels: one lane clears one word of a ring row (act_types words per key word)
+    if ((e->wide ? e->nkw > (uint32_t)e->nkw_t : e->nkw * act_types(e->compact) > 64) || e->nitems > 0x7FFFFFFFull * WPB ||
+        e->lds_bytes > 160 * 1024) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
         delete e;
         return BRC_E_INVALID;

@@ -127,7 +127,8 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // the key-list area doubles as the consensus phase's snapshot of every slot's (value, s + 1)
-    const uint32_t klist_u16 = (NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK;
+    // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
+    const uint32_t klist_u16 = ((NK + 2 * CHUNK) > ipw * NK ? (NK + 2 * CHUNK) : ipw * NK) * ((lean && !spec) ? 2u : 1u);
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
     const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;

@@ -37,8 +37,11 @@
 namespace brc {
 
 constexpr uint32_t NOKEY = 0xFFFFFFFFu;
-// lean key-list entries: key slot (< 2^12) | the message types that can land on it this step << TB_SH
+// lean key-list entries (u32): key slot (< 2^12) | the message types that can land on it this step << TB_SH
+// | for a SEND landing now: its sender << KL_SND_SH, its link delay - 1 << KL_DT_SH, KL_RESTR for a
+// restricted SEND -- everything the key loop needs from the slot's metadata
 constexpr uint32_t TB_S = 1, TB_E = 2, TB_R = 4, TB_SH = 12, TB_KEY = (1u << TB_SH) - 1u;
+constexpr uint32_t KL_SND_SH = 15, KL_DT_SH = 21, KL_RESTR = 1u << 25;
 
 template <int NPAD> struct MaskOf { using type = uint64_t; };
 template <> struct MaskOf<4> { using type = uint8_t; };
@@ -111,13 +114,17 @@ template <int NPAD, typename T> __device__ __forceinline__ T seg_or(T x) {
 
 __device__ __forceinline__ uint32_t hibit(uint32_t x) { return x ? 32u - (uint32_t)__clz(x) : 0u; }
 
-// Slot groups of G in {2, 4, 8} consecutive bits of a 64-bit key word: fold_groups leaves bit G*i set
-// iff group i has a set bit; compress_groups packs those bits (multiples of G) to bits 0 .. 64/G - 1.
+// Slot groups of G in {2, 4, 8, 16, 32} consecutive bits of a 64-bit key word: fold_groups leaves bit
+// G*i set iff group i has a set bit; compress_groups packs those bits (multiples of G) to bits 0 .. 64/G - 1.
 __device__ __forceinline__ uint64_t fold_groups(uint64_t x, uint32_t G) {
     if (G == 2) return (x | (x >> 1)) & 0x5555555555555555ull;
     if (G == 4) return (x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111111111111111ull;
     x |= x >> 1; x |= x >> 2; x |= x >> 4;
-    return x & 0x0101010101010101ull;
+    if (G == 8) return x & 0x0101010101010101ull;
+    x |= x >> 8;
+    if (G == 16) return x & 0x0001000100010001ull;
+    x |= x >> 16;
+    return x & 0x0000000100000001ull;
 }
 __device__ __forceinline__ uint64_t compress_groups(uint64_t x, uint32_t G) {
     if (G == 2) {
@@ -130,8 +137,15 @@ __device__ __forceinline__ uint64_t compress_groups(uint64_t x, uint32_t G) {
         x = (x | (x >> 12)) & 0x000000FF000000FFull;
         return (x | (x >> 24)) & 0xFFFFull;
     }
-    x = (x | (x >> 7)) & 0x0003000300030003ull; x = (x | (x >> 14)) & 0x0000000F0000000Full;
-    return (x | (x >> 28)) & 0xFFull;
+    if (G == 8) {
+        x = (x | (x >> 7)) & 0x0003000300030003ull; x = (x | (x >> 14)) & 0x0000000F0000000Full;
+        return (x | (x >> 28)) & 0xFFull;
+    }
+    if (G == 16) {
+        x = (x | (x >> 15)) & 0x0000000300000003ull;
+        return (x | (x >> 30)) & 0xFull;
+    }
+    return (x | (x >> 31)) & 0x3ull;
 }
 
 // compile-time unrolled loop: f(IC<0>{}), ..., f(IC<N-1>{}) (register arrays stay statically indexed)
@@ -323,16 +337,19 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #define BRC_MIN_WAVES 4      // waves per SIMD the register allocation must allow
 #endif
 #ifndef BRC_MIN_WAVES_LEAN
-#define BRC_MIN_WAVES_LEAN 5 // ... for the one-instance-per-wave (lean) instantiations
+#define BRC_MIN_WAVES_LEAN 4 // ... for the one-instance-per-wave (lean) instantiations: 128 VGPRs, no spills
+#endif                       // (A/B round 4: 162.7 ms vs 168.1 ms at 5 waves, which spill 32 VGPRs)
+#ifndef BRC_MIN_WAVES_LEAN_SPEC
+#define BRC_MIN_WAVES_LEAN_SPEC 5 // lean SPEC: its LDS (9.2 KB per wave) bounds residency near 17 waves per CU
 #endif
 #ifndef BRC_SPEC_MULTI
 #define BRC_SPEC_MULTI 1     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
 #endif
+#ifndef BRC_DACC
+#define BRC_DACC 1           // lean REFERENCE: deliveries collected per key word in a register (0: LDS atomics)
+#endif
 #ifndef BRC_PK
 #define BRC_PK 1             // lean kernels: a key pair's cell updates in the two 16-bit halves of a register
-#endif
-#ifndef BRC_LAZY_META
-#define BRC_LAZY_META 0      // lean kernels: key metadata read only for pairs with a SEND arrival (A/B: +1 %)
 #endif
 
 // Two u16 lanes per register (v_pk_*_u16): the lean kernels update the cells of a key PAIR with one
@@ -367,7 +384,9 @@ __device__ unsigned long long brc_stamps[BRC_NSTAMPS];
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
 
 template <int NPAD, int DM, bool EV, int MODE, int NLR>
-__global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? BRC_MIN_WAVES_LEAN : BRC_MIN_WAVES))
+__global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? (MODE == BRC_MODE_SPEC ? BRC_MIN_WAVES_LEAN_SPEC
+                                                                                          : BRC_MIN_WAVES_LEAN)
+                                                                : BRC_MIN_WAVES))
 void brc_step(const Params* __restrict__ pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
@@ -413,6 +432,9 @@ void brc_step(const Params* __restrict__ pp) {
     // gen | GEN16_RESTRICTED (lean kernels keep no generations: no area)
     uint16_t* s_gen = (uint16_t*)(s_dbits + dbw + h_words + l_words);
     uint16_t* s_klist = s_gen + (LEAN ? 0u : ((IPW * NK + 3) & ~3u));        // this step's active key slots
+    // lean REFERENCE / BEB: u32 entries (KL_*); lean SPEC keeps u16 entries (its LDS bounds its residency)
+    constexpr bool KL32 = LEAN && !SPEC;
+    uint32_t* s_klist32 = (uint32_t*)s_klist;
     // consensus phase: the key list is dead, and its area holds snap[IPW*NK] = value << 14 | (s + 1) of
     // every slot as the BRB phase left it.  A replica's phase change reallocates its own slot
     // mid-loop (send_key), while another replica may still have to count a delivery of the old key
@@ -714,15 +736,8 @@ void brc_step(const Params* __restrict__ pp) {
         vcount = 0; nvals = 0; order = 0;
         for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
     };
-    // :53-106 for a message of `host` carrying value id v (a BRB delivery, or BRC_INJ_DELIVER)
-    auto cons_deliver_vh = [&](uint32_t v, uint32_t host) {
-        // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
-        const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
-        const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
-        const bool found = (~(x | (x >> 1)) & 0x55u & valid) != 0;
-        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
-        s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
-        ++vcount;                                                    // :61
+    // :71-106: the phase ends a delivery may complete (value_count has just grown)
+    auto cons_after = [&]() {
         if (vcount >= P.T_cnt && phase == 1) {                       // :71
             const uint32_t prop = get_max_val(P.bound_p1);           // :73
             phase = 2; cons_reset();                                 // :75-78
@@ -738,6 +753,17 @@ void brc_step(const Params* __restrict__ pp) {
             ++round; phase = 1; cons_reset();                        // :96-100
             send_key(2 * (round - 1), dec);                          // :102-106
         }
+    };
+    // :53-106 for a message of `host` carrying value id v (a BRB delivery, or BRC_INJ_DELIVER)
+    auto cons_deliver_vh = [&](uint32_t v, uint32_t host) {
+        // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
+        const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
+        const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
+        const bool found = (~(x | (x >> 1)) & 0x55u & valid) != 0;
+        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
+        s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
+        ++vcount;                                                    // :61
+        cons_after();
     };
     auto cons_deliver = [&](uint32_t k) {
         cons_deliver_vh((uint32_t)s_snap[mbase + k] >> 14, k >> ksh);   // snapshot (see s_snap)
@@ -797,7 +823,7 @@ void brc_step(const Params* __restrict__ pp) {
     // BRC_INJ_MSG: this lane (the record's node) broadcasts ECHO / READY of key r.slot; true if the
     // message travels (sender peers: not a duplicate; connection peers: always)
     auto msg_cell = [&](const InjDev& r) -> bool {
-        const uint32_t k = r.slot;
+        const uint32_t k = LEAN ? uni32(r.slot) : r.slot;   // lean: records are wave-uniform (IPW = 1)
         bool sent = false;
         const uint64_t m = s_meta[mbase + k];
         if (m_s1(m) != r.s + 1u) {
@@ -937,7 +963,7 @@ void brc_step(const Params* __restrict__ pp) {
                         }
                     }
                     if constexpr (LEAN) {
-                        if (__ballot(fresh)) cst(k, C32_FRESH);
+                        if (__ballot(fresh)) cst(uni32(k), C32_FRESH);
                     }
                     q_until = max(q_until, t + hibit(os));
                 }
@@ -1069,10 +1095,23 @@ void brc_step(const Params* __restrict__ pp) {
             }
             const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
-            if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)((w * 64 + lane) | (tb << TB_SH));
+            if constexpr (KL32) {
+                if ((bits >> lane) & 1) {
+                    const uint64_t m = s_meta[w * 64 + lane];
+                    const uint32_t sx = (tb & TB_S) ? (((m_sender(m) & 63u) << KL_SND_SH) |
+                                                       (((t - m_tsend(m) - 1u) & 15u) << KL_DT_SH) |
+                                                       ((m & M_RESTRICTED) ? KL_RESTR : 0u)) : 0u;
+                    s_klist32[nkeys + below] = (w * 64 + lane) | (tb << TB_SH) | sx;
+                }
+            } else {
+                if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)((w * 64 + lane) | (tb << TB_SH));
+            }
             nkeys += (uint32_t)__popcll(bits);
         }
-        if (lane < 2 * CHUNK) s_klist[nkeys + lane] = (uint16_t)NK;   // chunk padding -> the trash row
+        if (lane < 2 * CHUNK) {                                   // chunk padding -> the trash row
+            if constexpr (KL32) s_klist32[nkeys + lane] = NK;
+            else s_klist[nkeys + lane] = (uint16_t)NK;
+        }
         if constexpr (LEAN) nk_lean += nkeys;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(0);
@@ -1122,12 +1161,14 @@ void brc_step(const Params* __restrict__ pp) {
                 return c;
             }
         };
+        // mk_a / mk_v (NLR): this lane's ring mark for the pair (LDS word, bit; mk_a = NOKEY: none), issued
+        // by the caller after the next chunk's key ids are read, so that read never waits for the mark
         auto process_pair = [&](const uint32_t (&ent)[2], const uint64_t (&m)[2], const uint32_t (&lo)[2],
-                                uint32_t (&nw)[2], bool (&wr)[2]) {
+                                uint32_t (&nw)[2], bool (&wr)[2], uint32_t& mk_a, uint64_t& mk_v) {
             uint32_t k[2], tb[2], tE[2], tR[2], ea[2] = {0u, 0u}, ra[2] = {0u, 0u}, sa[2] = {0u, 0u};
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                k[i] = ent[i] & TB_KEY; tb[i] = ent[i] >> TB_SH;
+                k[i] = ent[i] & TB_KEY; tb[i] = (ent[i] >> TB_SH) & 7u;
                 // lanes that are not real replicas and Byzantine lanes never update their cells here, so
                 // their words keep the fresh row's "never sent" unless an injection sent for them
                 tE[i] = (lo[i] >> C32_OE_SH) & 127u; tR[i] = lo[i] >> C32_OR_SH;   // offsets: SENT ECHO / READY
@@ -1143,8 +1184,12 @@ void brc_step(const Params* __restrict__ pp) {
                     if (tb[i] & TB_S) {
                         // SEND from the key's origin: lands on d iff delay(origin -> d) == t - t_send, and
                         // the key list holds the key now only for such a delay of the origin's outset
-                        const uint64_t mi = uni64(m[i]);                 // the row is wave-uniform
-                        const uint32_t dt = t - m_tsend(mi), snd = m_sender(mi);
+                        // sender, delay and restriction of the SEND: from the key-list entry (KL32) or
+                        // the key's metadata (the row is wave-uniform)
+                        const uint64_t mi = KL32 ? 0ull : uni64(m[i]);
+                        const uint32_t dt = KL32 ? ((ent[i] >> KL_DT_SH) & 15u) + 1u : t - m_tsend(mi);
+                        const uint32_t snd = KL32 ? (ent[i] >> KL_SND_SH) & 63u : m_sender(mi);
+                        const bool restr = KL32 ? (ent[i] & KL_RESTR) != 0 : (mi & M_RESTRICTED) != 0;
                         bool hit;
                         if constexpr (NLR != 0) {
                             hit = (((RL0 >> snd) & 1) != 0) == (dt == dly0);
@@ -1153,7 +1198,7 @@ void brc_step(const Params* __restrict__ pp) {
                             hit = (s_L[sj * 64 + lane] >> snd) & 1;
                         }
                         uint64_t hm = __ballot(hit) & hon_mask;
-                        if (mi & M_RESTRICTED) hm &= __ballot((gp(P.kdst)[inst * NK + k[i]] >> d) & 1ull);
+                        if (restr) hm &= __ballot((gp(P.kdst)[inst * NK + k[i]] >> d) & 1ull);
                         sa[i] = lane_in(hm) ? 1u : 0u;
                     }
                 }
@@ -1169,7 +1214,7 @@ void brc_step(const Params* __restrict__ pp) {
                 // a delivered cell ignores everything (core/brbroadcast.py:74): only open cells change
                 ob[i] = hb & ~__ballot((lo[i] & F_DEL) != 0);
             }
-            st_arr += lane_in(hon_mask) ? arr2 : 0u;
+            st_arr += arr2;                                      // non-honest lanes are dropped at the end
             if (!(ob[0] | ob[1])) return;                        // no open cell receives anything now
             BRC_KCOUNT(3);
             // Per-lane work below is branch-free integer arithmetic on 0/1 flags; a stage runs only
@@ -1331,7 +1376,7 @@ void brc_step(const Params* __restrict__ pp) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
                     if (db[i]) {
-                        if constexpr (DBG) {
+                        if constexpr (LEAN && (DBG || BRC_DACC)) {
                             // keys come in ascending slot order: a word is complete when the next word starts
                             const uint32_t wk = k[i] >> 6;
                             if (wk != dcur) {
@@ -1364,7 +1409,7 @@ void brc_step(const Params* __restrict__ pp) {
                     const bool lk1 = lane_in(0xF0F0F0F0F0F0F0F0ull), lty = lane_in(0xCCCCCCCCCCCCCCCCull);
                     const uint64_t sm = (lk1 ? (lty ? rb[1] : eb[1]) : (lty ? rb[0] : eb[0])) & mk_ov;
                     const uint32_t kx = lk1 ? k[1] : k[0];
-                    if (lane < 8 && sm != 0) atomicOr((unsigned long long*)&s_act[mk_row + (kx >> 6)], 1ull << (kx & 63));
+                    if (lane < 8 && sm != 0) { mk_a = mk_row + (kx >> 6); mk_v = 1ull << (kx & 63); }
                 } else {
 #pragma unroll
                     for (int i = 0; i < 2; ++i) {
@@ -1521,7 +1566,7 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
         };
-        // lean key pipeline registers; declared here so they stay live to the end of the step (below)
+        // lean key pipeline registers
         uint32_t w[CHUNK];                   // lean: compact cell words in flight
         uint32_t kk[CHUNK];
         if constexpr (LEAN) {
@@ -1530,7 +1575,7 @@ void brc_step(const Params* __restrict__ pp) {
             // p + c + CHUNK, so CHUNK cell loads stay in flight.  The chunk's key metadata is read
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
-            auto kid = [&](uint32_t p) { return uni32(s_klist[p]); };
+            auto kid = [&](uint32_t p) { return uni32(KL32 ? s_klist32[p] : (uint32_t)s_klist[p]); };
             auto cell = [&](uint32_t e) { return cld(e & TB_KEY); };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
@@ -1544,13 +1589,21 @@ void brc_step(const Params* __restrict__ pp) {
                 uint64_t mm[CHUNK];
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    // LAZY_META: the metadata is read only where the pair uses it (SEND arrivals, event log)
-                    mm[c] = (EV || !BRC_LAZY_META || ((kk[c] >> TB_SH) & TB_S)) ? s_meta[kk[c] & TB_KEY] : 0ull;
+                    // KL32: only the event log needs the key's metadata (phase index and value)
+                    mm[c] = (EV || !KL32) ? s_meta[kk[c] & TB_KEY] : 0ull;
                 });
-                // the refill key ids p + CHUNK .. p + 2 CHUNK - 1 in one 8-B read (p % 4 == 0 and
-                // s_klist is 8-B aligned), so a refill never waits on an LDS round trip of its own
-                static_assert(CHUNK == 4, "four u16 key ids per 8-B read");
-                const uint64_t knext = *(const uint64_t*)&s_klist[p + CHUNK];
+                // the refill entries p + CHUNK .. p + 2 CHUNK - 1 in 8-B reads (p % 4 == 0 and s_klist is
+                // 8-B aligned), so a refill never waits on an LDS round trip of its own
+                static_assert(CHUNK == 4, "four key-list entries per refill");
+                uint64_t knext[2];
+                if constexpr (KL32) {
+                    knext[0] = *(const uint64_t*)&s_klist32[p + CHUNK];
+                    knext[1] = *(const uint64_t*)&s_klist32[p + CHUNK + 2];
+                } else {
+                    const uint64_t k4 = *(const uint64_t*)&s_klist[p + CHUNK];
+                    knext[0] = (k4 & 0xFFFFull) | ((k4 & 0xFFFF0000ull) << 16);
+                    knext[1] = ((k4 >> 32) & 0xFFFFull) | ((k4 >> 48) << 32);
+                }
                 Unrolled<CHUNK / 2>::run([&](auto ci) {
                     constexpr int c = 2 * decltype(ci)::value;
                     // a pair past the list is skipped; the second key of a pair at the list's end is
@@ -1560,13 +1613,20 @@ void brc_step(const Params* __restrict__ pp) {
                     const uint32_t lo[2] = {w[c], w[c + 1]};
                     uint32_t nw[2] = {w[c], w[c + 1]};
                     bool wr[2] = {false, false};
-                    if (p + c < nkeys) process_pair(ent, mp, lo, nw, wr);
+                    uint32_t mk_a = NOKEY;
+                    uint64_t mk_v = 0;
+                    if (p + c < nkeys) process_pair(ent, mp, lo, nw, wr, mk_a, mk_v);
                     if (wr[0]) cst(kk[c] & TB_KEY, nw[0]);
                     if (wr[1]) cst(kk[c + 1] & TB_KEY, nw[1]);
-                    kk[c] = (uint32_t)(uni64(knext) >> (16 * c)) & 0xFFFFu;
-                    w[c] = cell(kk[c]);
-                    kk[c + 1] = (uint32_t)(uni64(knext) >> (16 * (c + 1))) & 0xFFFFu;
-                    w[c + 1] = cell(kk[c + 1]);
+                    // refill (none after the last chunk: no load is left in flight past the loop, so the
+                    // code after it neither waits for one nor keeps its registers)
+                    if (p + CHUNK < nkeys) {
+                        kk[c] = uni32((uint32_t)knext[c / 2]);
+                        w[c] = cell(kk[c]);
+                        kk[c + 1] = uni32((uint32_t)(knext[c / 2] >> 32));
+                        w[c + 1] = cell(kk[c + 1]);
+                    }
+                    if (mk_a != NOKEY) atomicOr((unsigned long long*)&s_act[mk_a], mk_v);
                 });
             }
         } else {
@@ -1672,17 +1732,20 @@ void brc_step(const Params* __restrict__ pp) {
                     // at once: the value sets gain the hosts (an origin is Q * NV consecutive slots),
                     // vcount the count, and values new to `order` enter by first slot (= delivery order).
                     // The others (a phase change, or two phases of one key in one step) go one by one.
+                    // A phase change inside the word splits it: the prefix (in delivery order) that
+                    // completes the phase goes at once, then the phase ends (cons_after), then the rest.
                     if (__ballot(bits != 0)) {
                         const uint32_t sv = (uint32_t)s_snap[w * 64 + lane] >> 14;   // slot w*64+lane's value
                         const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
-                        const uint32_t nb = (uint32_t)__popcll(bits);
+                        uint32_t nb = (uint32_t)__popcll(bits);
                         const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
-                        if (nb && oneper && ((phase != 1 && phase != 2) || vcount + nb < P.T_cnt)) {
+                        // the deliveries of `part` (a subset of this word's, one per key prefix) at once
+                        auto bulk = [&](uint64_t part) {
                             const uint32_t G = Q * NV, opw = 64u / G;
                             uint32_t first[4];
 #pragma unroll
                             for (int v = 0; v < 4; ++v) {
-                                const uint64_t dv = bits & vm[v];
+                                const uint64_t dv = part & vm[v];
                                 first[v] = dv ? (uint32_t)__ffsll((unsigned long long)dv) - 1u : 64u;
                                 if (dv) s_hm[v * 64 + lane] |= (T)(compress_groups(fold_groups(dv, G), G) << (w * opw));
                                 // already inserted? (the field test of cons_deliver_vh)
@@ -1698,8 +1761,29 @@ void brc_step(const Params* __restrict__ pp) {
 #pragma unroll
                                 for (int v = 0; v < 4; ++v) if ((uint32_t)v == bv) first[v] = 64u;   // static indices
                             }
-                            vcount += nb;
-                            bits = 0;
+                        };
+                        while (nb && oneper) {
+                            if ((phase != 1 && phase != 2) || vcount + nb < P.T_cnt) {
+                                bulk(bits);
+                                vcount += nb;
+                                bits = 0;
+                                break;
+                            }
+                            // the deliveries up to the one that completes the phase: the lowest `need` bits
+                            const uint32_t need = vcount >= P.T_cnt ? 1u : P.T_cnt - vcount;
+                            uint64_t x = bits;
+                            uint32_t kth = need, pos = 0;
+#pragma unroll
+                            for (uint32_t sh = 32; sh; sh >>= 1) {      // position of the need-th set bit
+                                const uint32_t c = (uint32_t)__popcll(x & ((1ull << sh) - 1ull));
+                                if (kth > c) { kth -= c; x >>= sh; pos += sh; }
+                            }
+                            const uint64_t pre = bits & (pos >= 63 ? ~0ull : ((2ull << pos) - 1ull));
+                            bulk(pre);
+                            vcount += need;
+                            bits &= ~pre;
+                            nb -= need;
+                            cons_after();                                 // :71-106
                         }
                     }
                 }
@@ -1754,13 +1838,6 @@ void brc_step(const Params* __restrict__ pp) {
         }
         if ((uint32_t)lane < nkw * AT) s_act[row * nkw * AT + lane] = 0;
         any_rows &= ~(1u << row);
-        if constexpr (LEAN) {
-            // The key loop's last refills load past the list (trash row) and nothing reads them;
-            // a use here keeps their registers from being reused by the consensus and action code
-            // above, which would otherwise wait for those loads right after the key loop.
-#pragma unroll
-            for (int c = 0; c < CHUNK; ++c) asm volatile("" ::"v"(w[c]));
-        }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(4);
     }
@@ -1803,6 +1880,7 @@ void brc_step(const Params* __restrict__ pp) {
         }
     }
     if (LEAN && lane != 0) { st_cells = 0; st_del = 0; st_bcast = 0; }   // lean: wave-uniform counts
+    if (LEAN && !honest) st_arr = 0;             // lean: arrivals were summed on every lane
     st_msgs += st_bcast * n;
     if (LEAN && real) st_loads += nk_lean - nk_skip;
     // statistics: reduce over the segment, its leader writes the instance row

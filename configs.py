@@ -97,14 +97,30 @@ def measured_traffic(name, kernel_ms):
     return best
 
 
-def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0):
+def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0, kernel="step"):
     """HBM fractions of the dominant kernel, as bench.py reports them: `frac` prices this layout's
     algorithmic bytes (the cell word read + written per cell-step), `survey_model_frac` SURVEY
-    §8(d)'s n-bit-mask model, `traffic_frac` the rocprofv3 counters of a committed profile."""
+    §8(d)'s n-bit-mask model, `traffic_frac` the rocprofv3 counters of a committed profile.
+    kernel: Engine.last_kernel() of the run -- the key-lifetime kernel ("life") moves no cell bytes,
+    so it is reported as issue-bound with no HBM fraction (bench.py does the same)."""
     sec = kernel_ms / 1e3
+    if kernel not in ("step", "life"):
+        raise ValueError("%s: launches ran different kernels (%r); report them apart" % (name, kernel))
+    if kernel == "life":
+        out = {"bound": "issue", "kernel": "brc_life", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": None,
+               "frac": None, "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS,
+               "cell_steps_per_s": cell_steps / sec, "traffic": None, "traffic_frac": None,
+               "note": "key-lifetime kernel: cells stay in registers for a key's lifetime, no HBM cell traffic; "
+                       "survey_model_frac prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
+        t = measured_traffic(name, kernel_ms)
+        if t:
+            out["traffic"], out["traffic_source"] = t
+            out["traffic_frac"] = t[0] / sec / 1e9 / HBM_PEAK_GBS
+        return out
     floor_b = 2 * cell_bytes(n, peer_mode)
     achieved = floor_b * cell_steps / sec / 1e9
-    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": achieved,
+    out = {"bound": "hbm", "kernel": "brc_step" if n <= 64 else "brc_step_wide", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "achieved": achieved,
            "frac": achieved / HBM_PEAK_GBS, "bytes_per_unit": floor_b,
            "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS, "cell_bytes": floor_b // 2,
            "traffic": None, "traffic_frac": None,
@@ -160,11 +176,12 @@ def main():
                 eng.run()
             barrier()
             t0 = time.perf_counter()
-            kms = []
+            kms, kern = [], set()
             for _ in range(args.steps):
                 eng.reset()
                 eng.run()
                 kms.append(eng.last_kernel_ms())
+                kern.add(eng.last_kernel())
             barrier()
             elapsed = time.perf_counter() - t0
             st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(66))
@@ -182,7 +199,9 @@ def main():
                 "statuses": {k: st[k] for k in ("done", "quiescent", "stepcap", "overflow", "running")},
                 "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
                 "cell_steps_per_launch": st["cell_steps"], "lane_loads_per_launch": st["lane_loads"],
-                "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms, kw.get("peer_mode", 0)),
+                "kernel": kern.pop() if len(kern) == 1 else "mixed",
+                "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms, kw.get("peer_mode", 0),
+                                     kernel=next(iter(kern)) if len(kern) == 1 else "mixed"),
             }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -90,8 +90,10 @@ typedef struct {
     uint32_t delay_const;     /* BRC_DELAY_CONST value */
     uint32_t round_cap;       /* consensus: instance DONE when every honest replica decided this many times */
     uint32_t step_cap;        /* last simulated step (<= 60000) */
-    uint32_t key_window;      /* Q: live phase indices per origin (2, 4 or 8) */
-    uint32_t variants;        /* NV: key variants per origin (1, 2 or 4; Q*NV <= 8) */
+    uint32_t key_window;      /* Q: live phase indices per origin (2, 4, 8; 16 or 32 with n <= 64 and the
+                                 reference / best-effort protocols, whose phase leakage keeps up to ~17
+                                 phases of one origin in flight by round 8 under slow-set D = 8) */
+    uint32_t variants;        /* NV: key variants per origin (1, 2 or 4; Q*NV <= 8, <= 32 where Q may be) */
     uint32_t proposals;       /* BRC_PROPOSALS_* (consensus) */
     uint32_t byz_pattern;     /* BRC_BYZ_* applied to every instance */
     uint32_t event_capacity;  /* 0: no event log */

@@ -31,6 +31,36 @@ def load_counters(src):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in per.items()}
 
 
+CUS, SIMDS, XCDS = 256, 1024, 8          # MI355X_MICROARCH.md chip parameters
+
+
+def issue_block(k):
+    """Instruction-issue view of one kernel from its PMC means (the kernels here are issue- and
+    latency-bound, not HBM-bound): VALU busy = SQ_INSTS_VALU x 2 cycles (a wave64 op on a SIMD-32)
+    over SIMDs x cycles, with cycles = GRBM_GUI_ACTIVE / 8 (summed over the XCDs); SALU and branch
+    instructions per CU-cycle; the wave-cycle split (SQ_WAVE_CYCLES and SQ_WAIT_* count quad-cycles)
+    and the mean resident waves per SIMD."""
+    need = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "GRBM_GUI_ACTIVE")
+    if not all(c in k for c in need) or not k["GRBM_GUI_ACTIVE"]:
+        return None
+    cyc = k["GRBM_GUI_ACTIVE"] / XCDS
+    out = {"cycles": cyc, "valu_insts": k["SQ_INSTS_VALU"], "salu_insts": k["SQ_INSTS_SALU"],
+           "valu_busy": k["SQ_INSTS_VALU"] * 2.0 / (SIMDS * cyc),
+           "salu_per_cu_cycle": k["SQ_INSTS_SALU"] / (CUS * cyc)}
+    if "SQ_INSTS_BRANCH" in k:
+        out["branch_per_cu_cycle"] = k["SQ_INSTS_BRANCH"] / (CUS * cyc)
+    if "SQ_INSTS_LDS" in k:
+        out["lds_insts"] = k["SQ_INSTS_LDS"]
+    wc = k.get("SQ_WAVE_CYCLES")
+    if wc:
+        out["waves_per_simd"] = wc * 4.0 / cyc / SIMDS
+        for c, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_inst_frac"),
+                        ("SQ_ACTIVE_INST_ANY", "active_frac")):
+            if c in k:
+                out[name] = k[c] / wc
+    return out
+
+
 def kernel_avg_ns(src, kernel):
     path = os.path.join(src, "trace", "run_kernel_stats.csv")
     for r in csv.DictReader(open(path)):
@@ -58,7 +88,7 @@ def main():
         shutil.copy(bpath, os.path.join(dest, "trace_bench.json"))
     k = counters.get(kernel, {})
     avg_ns, calls = kernel_avg_ns(src, kernel)
-    out = {"kernel": kernel, "avg_ns": avg_ns, "calls": calls, "source": dest}
+    out = {"kernel": kernel, "avg_ns": avg_ns, "calls": calls, "source": dest, "issue": issue_block(k)}
     if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
         fetch = 2.0 * k["FETCH_SIZE"] * 1024.0
         write = k["WRITE_SIZE"] * 1024.0

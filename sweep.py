@@ -5,6 +5,7 @@ with the nccl backend; one process per GPU).
 
     python sweep.py [--instances I] [--mode spec|reference] [--f 0,21,85] [--models const,uniform,geometric]
     python -m torch.distributed.run --nproc-per-node N ... sweep.py    (multi-GPU, weak scaling)
+    python -m torch.distributed.run --nproc-per-node 1 ... sweep.py --dist   (one RCCL rank)
 
 Every configuration is its own engine (one launch).  Instances shard across ranks by global id, so
 the histograms do not depend on the rank count.  Default mode is SPEC (the intended protocol with
@@ -25,7 +26,7 @@ N = 256
 SEED, COIN_SEED = 0x5EED0005, 0xC017C017
 MODELS = {"const": (0, 1), "uniform": (1, 4), "geometric": (3, 16)}   # (BRC_DELAY_*, delay_max)
 BINS = 66
-BYTES_PER_CELL_STEP = 6 * ((N + 7) // 8) + 2      # 194 B at n = 256
+BYTES_PER_CELL_STEP = 6 * ((N + 7) // 8) + 2      # 194 B at n = 256 (survey_model_frac)
 
 
 def parse():
@@ -37,6 +38,10 @@ def parse():
     ap.add_argument("--key-window", type=int, default=8)
     ap.add_argument("--round-cap", type=int, default=1)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the process group (and all-reduce the histograms) even at world size 1")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo rehearses ranks sharing one GPU")
     return ap.parse_args()
 
 
@@ -46,12 +51,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    coll_dev = "cuda"
+    if world > 1 or args.dist:
         import torch
         import torch.distributed as tdist
+        if args.backend == "gloo":
+            local %= torch.cuda.device_count()
+            coll_dev = "cpu"
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group("gloo")
         dist = tdist
+    import configs
     from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd import shard
     from byzantinerandomizedconsensus_amd.engine import Engine
@@ -71,9 +84,10 @@ def main():
                 eng.run()
                 t2 = time.perf_counter()
                 kms = eng.last_kernel_ms()
-                st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(BINS))
-            wall = shard.max_over_ranks(t2 - t1, dist, device="cuda")
-            kms = shard.max_over_ranks(kms, dist, device="cuda")
+                kernel = eng.last_kernel()
+                st, hist = shard.reduce_stats(eng.stats(), dist, device=coll_dev, hist=eng.round_histogram(BINS))
+            wall = shard.max_over_ranks(t2 - t1, dist, device=coll_dev)
+            kms = shard.max_over_ranks(kms, dist, device=coll_dev)
             if rank == 0:
                 decided = sum(hist[1:])
                 mean_r = sum(r * c for r, c in enumerate(hist) if r) / decided if decided else None
@@ -86,9 +100,12 @@ def main():
                     "round_hist": {str(r): c for r, c in enumerate(hist) if c}, "mean_decide_round": mean_r,
                     "max_decide_round": last, "msgs_sent": st["msgs_sent"], "arrivals": st["arrivals"],
                     "cell_steps": st["cell_steps"],
-                    "roofline": {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,
-                                 "achieved": BYTES_PER_CELL_STEP * st["cell_steps"] / world / (kms / 1e3) / 1e9,
-                                 "note": "algorithmic %d B per cell-step (SURVEY 8(d) at n=256)" % BYTES_PER_CELL_STEP},
+                    # the floor model bench.py and configs.py use: the cell word read + written per
+                    # cell-step (16 B on the wide kernel's 8-B cells); SURVEY 8(d)'s 194 B beside it
+                    "roofline": configs.roofline("cfg5-sweep", N, BYTES_PER_CELL_STEP, st["cell_steps"] / world, kms,
+                                                 kernel=kernel),
+                    "kernel": kernel, "collective": (dist.get_backend() + " all-reduce of the histograms")
+                    if dist is not None else None,
                     "kernel_ms": kms, "wall_ms": wall * 1e3, "setup_ms": (t1 - t0) * 1e3,
                     "decided_instances_per_s": decided / wall if wall else None}), flush=True)
     if dist is not None:

@@ -24,7 +24,8 @@ def sort_result(res):
 def _cfg_key(sp):
     return (sp["n"], sp["f"], sp["mode"], sp.get("nv", 1), sp["seed"], sp["delay_model"], sp["dmax"],
             sp.get("dconst", 1), sp.get("round_cap", 0), sp.get("step_cap", 10000),
-            tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"), sp.get("peer_mode", "sender"))
+            tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"), sp.get("peer_mode", "sender"),
+            sp.get("key_window"))
 
 
 def _injections(sp, local):
@@ -60,14 +61,15 @@ def _injections(sp, local):
 
 
 def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
-    """specs share _cfg_key and have consecutive g.  The key window defaults to the widest
-    the engine allows (Q * NV <= 8)."""
+    """specs share _cfg_key and have consecutive g.  The key window defaults to the spec's
+    "key_window" (reference-protocol runs of many rounds keep more phases of one origin in flight),
+    else 8 // nv."""
     sp0 = specs[0]
     spec_mode = sp0["mode"] in ("spec", "spec_brb")
     if spec_mode:
         key_window = sp0["window"]          # the SPEC buffering window IS the engine's key window
     elif key_window is None:
-        key_window = 8 // sp0.get("nv", 1)
+        key_window = sp0.get("key_window") or 8 // sp0.get("nv", 1)
     protocol = {"spec": "consensus", "spec_brb": "brb", "beb": "brb", "beb_consensus": "consensus"}.get(
         sp0["mode"], sp0["mode"])
     mode = L.MODE_SPEC if spec_mode else (L.MODE_BEB if sp0["mode"].startswith("beb") else L.MODE_REFERENCE)

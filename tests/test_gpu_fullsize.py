@@ -228,35 +228,32 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
 @pytest.mark.parametrize("mode", ["reference", "spec"])
 def test_cfg4_long_consensus_many_rounds(mode):
     """Long-running consensus at scale (the reference re-proposes forever,
-    core/byzantinerandomizedconsensus.py:96-106): 2^17 n=64 f=21 instances run to round_cap = 8
-    decisions per replica, so slots recycle and the compact cells' epoch moves across many rounds
-    under a full batch.  SPEC runs the cfg4 slow-set schedule (D = 8); the reference protocol runs
-    constant delays D = 2, because its fast replicas cycle rounds faster than a phase window of 8
-    covers the D = 8 slow set (BRC_OVERFLOW).  Sampled instances equal the oracle
-    (counters and every replica's first and last decision, values included)."""
+    core/byzantinerandomizedconsensus.py:96-106): 2^17 n=64 f=21 instances of the cfg4 slow-set
+    schedule (D = 8) run to round_cap = 8 decisions per replica, so slots recycle and the compact
+    cells' epoch moves across many rounds under a full batch.  The reference protocol's phase
+    leakage (:57-61, :71-78: deliveries of any phase count toward the current one) lets fast
+    replicas run ahead, so up to 17 phase indices of one origin are in flight by round 8: it runs
+    with a key window of 32 (SPEC needs 8).  Sampled instances equal the oracle (counters and every
+    replica's first and last decision, values included)."""
     L = _L()
     N, CAP = 1 << 17, 8
     spec = mode == "spec"
-    if spec:
-        kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
-                  round_cap=CAP, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX, mode=L.MODE_SPEC,
-                  coin_seed=0xC017C017)
-    else:
-        kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_CONST, delay_max=2,
-                  delay_const=2, round_cap=CAP, step_cap=4000, key_window=8, proposals=L.PROPOSALS_PHILOX)
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=CAP, step_cap=4000, key_window=8 if spec else 32, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
     ids = sorted(random.Random(8).sample(range(N), 6)) + [N - 1]
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
         res_all = eng.instances_result()
         res = {i: res_all[i] for i in ids}
         reps = {i: eng.replicas(i, 1)[0] for i in ids}
-    assert all(r["status"] == "done" for r in res_all)
+    assert all(r["status"] == "done" for r in res_all)      # no BRC_OVERFLOW
     for g in ids:
         if spec:
             exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8,
                                               coin_seed=0xC017C017))
         else:
-            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 0, 2, g, round_cap=CAP, dconst=2))
+            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP))
         for k in KEYS:
             assert res[g][k] == exp[k], (g, k)
         first, last, count = {}, {}, {}

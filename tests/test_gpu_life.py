@@ -42,6 +42,11 @@ def _workloads():
         # window overflows (both kernels stop with BRC_OVERFLOW at the same step)
         "ref-const64-cap30-ovf": dict(base, n=64, f=21, seed=0x5EED0034, delay_model=L.DELAY_CONST, delay_max=1,
                                       delay_const=1, round_cap=0, key_window=8, step_cap=30),
+        # ... which a key window of 32 covers (up to 27 phase indices of one origin in flight)
+        "ref-const64-cap30-q32": dict(base, n=64, f=21, seed=0x5EED0034, delay_model=L.DELAY_CONST, delay_max=1,
+                                      delay_const=1, round_cap=0, key_window=32, step_cap=30),
+        "ref-slow64-r6-q32": dict(base, n=64, f=21, seed=0x5EED0036, delay_model=L.DELAY_SLOWSET, delay_max=8,
+                                  round_cap=6, key_window=32),
         "ref-const64-r4": dict(base, n=64, f=21, seed=0x5EED0015, delay_model=L.DELAY_CONST, delay_max=2, delay_const=2,
                                round_cap=4, key_window=8),
         "spec-slow64": dict(base, n=64, f=21, seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8, round_cap=2,

@@ -340,8 +340,8 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #define BRC_MIN_WAVES_LEAN 4 // ... for the one-instance-per-wave (lean) instantiations: 128 VGPRs, no spills
 #endif                       // (A/B round 4: 162.7 ms vs 168.1 ms at 5 waves, which spill 32 VGPRs)
 #ifndef BRC_MIN_WAVES_LEAN_SPEC
-#define BRC_MIN_WAVES_LEAN_SPEC 5 // lean SPEC: its LDS (9.2 KB per wave) bounds residency near 17 waves per CU
-#endif
+#define BRC_MIN_WAVES_LEAN_SPEC 4 // lean SPEC: its LDS (9.2 KB per wave) bounds residency near 17 waves per CU
+#endif                            // anyway (A/B round 4: 295 ms at 4 vs 309 ms at 5 waves/SIMD)
 #ifndef BRC_SPEC_MULTI
 #define BRC_SPEC_MULTI 1     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
 #endif
@@ -441,7 +441,7 @@ void brc_step(const Params* __restrict__ pp) {
     // in that slot from this same step (its t_quiet may be this step): deliveries read the snapshot.
     uint16_t* s_snap = s_klist;
     // non-lean kernels: a window of the item's injection records, staged in LDS (INJ_CACHE at a time)
-    uint64_t* s_injc = (uint64_t*)(s_klist + ((max(NK + 2 * CHUNK, IPW * NK) + 3) & ~3u));
+    uint64_t* s_injc = (uint64_t*)(s_klist + ((max(NK + 2 * KPAD, IPW * NK) + 3) & ~3u));
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -1108,7 +1108,7 @@ void brc_step(const Params* __restrict__ pp) {
             }
             nkeys += (uint32_t)__popcll(bits);
         }
-        if (lane < 2 * CHUNK) {                                   // chunk padding -> the trash row
+        if (lane < 2 * KPAD) {                                    // chunk padding -> the trash row
             if constexpr (KL32) s_klist32[nkeys + lane] = NK;
             else s_klist[nkeys + lane] = (uint16_t)NK;
         }
@@ -1567,44 +1567,47 @@ void brc_step(const Params* __restrict__ pp) {
             }
         };
         // lean key pipeline registers
-        uint32_t w[CHUNK];                   // lean: compact cell words in flight
-        uint32_t kk[CHUNK];
+        uint32_t w[LCHUNK];                  // lean: compact cell words in flight
+        uint32_t kk[LCHUNK];
         if constexpr (LEAN) {
-            // software pipeline, unrolled by CHUNK so the in-flight cell words never move between
+            // software pipeline, unrolled by LCHUNK so the in-flight cell words never move between
             // registers: slot c holds key p + c; right after it is processed, slot c loads key
-            // p + c + CHUNK, so CHUNK cell loads stay in flight.  The chunk's key metadata is read
+            // p + c + LCHUNK, so LCHUNK cell loads stay in flight.  The chunk's key metadata is read
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(KL32 ? s_klist32[p] : (uint32_t)s_klist[p]); };
             auto cell = [&](uint32_t e) { return cld(e & TB_KEY); };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
-            Unrolled<CHUNK>::run([&](auto ci) {
+            Unrolled<LCHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 kk[c] = kid(c);
                 w[c] = cell(kk[c]);
                 __builtin_amdgcn_sched_barrier(0);
             });
-            for (uint32_t p = 0; p < nkeys; p += CHUNK) {
-                uint64_t mm[CHUNK];
-                Unrolled<CHUNK>::run([&](auto ci) {
+            for (uint32_t p = 0; p < nkeys; p += LCHUNK) {
+                uint64_t mm[LCHUNK];
+                Unrolled<LCHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     // KL32: only the event log needs the key's metadata (phase index and value)
                     mm[c] = (EV || !KL32) ? s_meta[kk[c] & TB_KEY] : 0ull;
                 });
-                // the refill entries p + CHUNK .. p + 2 CHUNK - 1 in 8-B reads (p % 4 == 0 and s_klist is
-                // 8-B aligned), so a refill never waits on an LDS round trip of its own
-                static_assert(CHUNK == 4, "four key-list entries per refill");
-                uint64_t knext[2];
-                if constexpr (KL32) {
-                    knext[0] = *(const uint64_t*)&s_klist32[p + CHUNK];
-                    knext[1] = *(const uint64_t*)&s_klist32[p + CHUNK + 2];
-                } else {
-                    const uint64_t k4 = *(const uint64_t*)&s_klist[p + CHUNK];
-                    knext[0] = (k4 & 0xFFFFull) | ((k4 & 0xFFFF0000ull) << 16);
-                    knext[1] = ((k4 >> 32) & 0xFFFFull) | ((k4 >> 48) << 32);
-                }
-                Unrolled<CHUNK / 2>::run([&](auto ci) {
+                // the refill entries p + LCHUNK .. p + 2 LCHUNK - 1 in 8-B reads (p % 4 == 0 and s_klist
+                // is 8-B aligned), so a refill never waits on an LDS round trip of its own
+                static_assert(LCHUNK == 4 || LCHUNK == 8, "four or eight key-list entries per refill");
+                uint64_t knext[LCHUNK / 2];           // entries 2i | 2i + 1 << 32
+                Unrolled<LCHUNK / 4>::run([&](auto qi) {
+                    constexpr int q = decltype(qi)::value;
+                    if constexpr (KL32) {
+                        knext[2 * q] = *(const uint64_t*)&s_klist32[p + LCHUNK + 4 * q];
+                        knext[2 * q + 1] = *(const uint64_t*)&s_klist32[p + LCHUNK + 4 * q + 2];
+                    } else {
+                        const uint64_t k4 = *(const uint64_t*)&s_klist[p + LCHUNK + 4 * q];
+                        knext[2 * q] = (k4 & 0xFFFFull) | ((k4 & 0xFFFF0000ull) << 16);
+                        knext[2 * q + 1] = ((k4 >> 32) & 0xFFFFull) | ((k4 >> 48) << 32);
+                    }
+                });
+                Unrolled<LCHUNK / 2>::run([&](auto ci) {
                     constexpr int c = 2 * decltype(ci)::value;
                     // a pair past the list is skipped; the second key of a pair at the list's end is
                     // the padding entry (the trash row, no message type): it changes nothing
@@ -1620,7 +1623,7 @@ void brc_step(const Params* __restrict__ pp) {
                     if (wr[1]) cst(kk[c + 1] & TB_KEY, nw[1]);
                     // refill (none after the last chunk: no load is left in flight past the loop, so the
                     // code after it neither waits for one nor keeps its registers)
-                    if (p + CHUNK < nkeys) {
+                    if (p + LCHUNK < nkeys) {
                         kk[c] = uni32((uint32_t)knext[c / 2]);
                         w[c] = cell(kk[c]);
                         kk[c + 1] = uni32((uint32_t)(knext[c / 2] >> 32));

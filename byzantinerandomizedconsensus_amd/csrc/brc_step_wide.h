@@ -27,6 +27,10 @@
 #pragma once
 #include "brc_step.h"
 
+#ifndef BRC_WIDE_MSTORE
+#define BRC_WIDE_MSTORE 1    // exec-masked cell stores (0: whole-row stores, unchanged words written back)
+#endif
+
 namespace brc {
 
 // waves per SIMD the register allocation must allow (<= 168 VGPRs at 3): with generation-free cells
@@ -798,7 +802,11 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
                 const uint32_t tEn = es ? t : tE, tRn = rs ? t : tR;
                 const uint64_t nw = (uint64_t)fl | ((uint64_t)min(ec, 255u) << 5) | ((uint64_t)min(rc, 255u) << 13) |
                                     ((uint64_t)tEn << 32) | ((uint64_t)tRn << 48);
+#if BRC_WIDE_MSTORE
+                if (has) mycells[(size_t)k * (CW * NPAD)] = nw;  // only cells with arrivals change (exec-masked)
+#else
                 mycells[(size_t)k * (CW * NPAD)] = has ? nw : wd;
+#endif
             }
             st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
             st_cells += has ? 1u : 0u;

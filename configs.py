@@ -15,7 +15,7 @@ Workloads:
   cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^20 instances per GPU
   cfg4-conn  the same with connection-identity peers (what the shipped reference runs), 2^18
   cfg4-beb   the reference consensus over best-effort broadcast (BRC_MODE_BEB), 2^20
-  cfg5-*     n=256 f=85 SPEC, 2048 instances per GPU, const / uniform[1,4] / geometric<=16
+  cfg5-*     n=256 f=85 SPEC, 6144 instances per GPU, const / uniform[1,4] / geometric<=16
 
 A step is one pass of the hot path over the batch (reset + run to completion); the timed region
 is K steps between barriers, max over ranks.  `roofline.achieved` = this layout's algorithmic
@@ -64,7 +64,8 @@ def workloads(L):
     W["cfg4-beb"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                          round_cap=1, key_window=8, mode=L.MODE_BEB))
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
-        W["cfg5-" + name] = (2048, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
+        # 6,144 instances per GPU: 8 waves of the 768 resident workgroups (3 per CU), so no partial last wave
+        W["cfg5-" + name] = (6144, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
                                              delay_max=dmax, round_cap=1, key_window=8, mode=L.MODE_SPEC,
                                              coin_seed=COIN_SEED))
     return W
@@ -187,6 +188,7 @@ def main():
             st, hist = shard.reduce_stats(eng.stats(), dist, device="cuda", hist=eng.round_histogram(66))
         elapsed = shard.max_over_ranks(elapsed, dist, device="cuda")
         kernel_ms = shard.max_over_ranks(sum(kms) / len(kms), dist, device="cuda")
+        kname = next(iter(kern)) if len(kern) == 1 else "mixed"
         if rank == 0:
             print(json.dumps({
                 "workload": name, "n": n, "f": kw["f"], "instances": st["instances"], "n_gpus": world,
@@ -199,9 +201,9 @@ def main():
                 "statuses": {k: st[k] for k in ("done", "quiescent", "stepcap", "overflow", "running")},
                 "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
                 "cell_steps_per_launch": st["cell_steps"], "lane_loads_per_launch": st["lane_loads"],
-                "kernel": kern.pop() if len(kern) == 1 else "mixed",
+                "kernel": kname,
                 "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms, kw.get("peer_mode", 0),
-                                     kernel=next(iter(kern)) if len(kern) == 1 else "mixed"),
+                                     kernel=kname),
             }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -123,17 +123,16 @@ constexpr uint32_t INJ_CACHE = 16;
 
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][act_types][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
-// mgen[IPW*NK] u16 (not on the lean kernels) | klist[max(NK + 2 CHUNK, IPW*NK)] u16 (tail padded with the trash row NK;
-// reused as the consensus snapshot snap[IPW*NK] u16) | injc[INJ_CACHE][3] u64 (not on the lean kernels)
+// mgen[IPW*NK] u16 (not on the lean kernels) | klist[NK + 2 KPAD] u16 (tail padded with the trash row NK;
+// u32 entries on the lean REFERENCE / BEB kernels) | injc[INJ_CACHE][3] u64 (not on the lean kernels)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
-    // the key-list area doubles as the consensus phase's snapshot of every slot's (value, s + 1)
     // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
-    const uint32_t klist_u16 = ((NK + 2 * KPAD) > ipw * NK ? (NK + 2 * KPAD) : ipw * NK) * ((lean && !spec) ? 2u : 1u);
+    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && !spec) ? 2u : 1u);
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
     const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;

@@ -345,6 +345,18 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #ifndef BRC_SPEC_MULTI
 #define BRC_SPEC_MULTI 1     // lean SPEC consensus: a key word's deliveries at once per distinct phase index
 #endif
+#ifndef BRC_PERKEY_CNT
+#define BRC_PERKEY_CNT 1     // lean kernels: arrival counts per key of a pair only where that key's entry has the type (A/B: -0.8 %)
+#endif
+#ifndef BRC_BRANCHLESS
+#define BRC_BRANCHLESS 0     // lean kernels: ECHO / READY stages of a pair evaluated whether or not they can land
+#endif
+#ifndef BRC_NOEARLY
+#define BRC_NOEARLY 0        // lean kernels: no early exit for pairs that reach no open cell
+#endif
+#ifndef BRC_LCHUNK_SPEC
+#define BRC_LCHUNK_SPEC 4    // lean SPEC: key slots in flight per chunk (8 spills two VGPRs there)
+#endif
 #ifndef BRC_DACC
 #define BRC_DACC 1           // lean REFERENCE: deliveries collected per key word in a register (0: LDS atomics)
 #endif
@@ -376,9 +388,10 @@ __device__ __forceinline__ uint32_t pk2(uint32_t x) { return x | (x << 16); }   
 // metadata read once per chunk, exec-masked cell stores and (NLR = 2) link-delay masks held in
 // registers -- the headline configuration has exactly two link delays.
 #ifdef BRC_STAMPS
-#define BRC_NSTAMPS 9
-// dev-only: [0..4] section timers (s_memtime ticks); [5..8] lean key-steps: processed, without
-// arrivals, reaching only delivered cells, fully updated
+#define BRC_NSTAMPS 12
+// dev-only: [0..7] section timers (s_memtime ticks): step head + key list, key loop, consensus
+// words, actions, stop checks, consensus snapshot, consensus row clears, key-loop tail (ring rows);
+// [8..11] lean key-steps: processed, without arrivals, reaching only delivered cells, fully updated
 __device__ unsigned long long brc_stamps[BRC_NSTAMPS];
 #endif
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
@@ -435,13 +448,8 @@ void brc_step(const Params* __restrict__ pp) {
     // lean REFERENCE / BEB: u32 entries (KL_*); lean SPEC keeps u16 entries (its LDS bounds its residency)
     constexpr bool KL32 = LEAN && !SPEC;
     uint32_t* s_klist32 = (uint32_t*)s_klist;
-    // consensus phase: the key list is dead, and its area holds snap[IPW*NK] = value << 14 | (s + 1) of
-    // every slot as the BRB phase left it.  A replica's phase change reallocates its own slot
-    // mid-loop (send_key), while another replica may still have to count a delivery of the old key
-    // in that slot from this same step (its t_quiet may be this step): deliveries read the snapshot.
-    uint16_t* s_snap = s_klist;
     // non-lean kernels: a window of the item's injection records, staged in LDS (INJ_CACHE at a time)
-    uint64_t* s_injc = (uint64_t*)(s_klist + ((max(NK + 2 * KPAD, IPW * NK) + 3) & ~3u));
+    uint64_t* s_injc = (uint64_t*)(s_klist + ((NK + 2 * KPAD + 3) & ~3u));
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -711,7 +719,7 @@ void brc_step(const Params* __restrict__ pp) {
     };
     // honest origin d broadcasts SEND for its key (d, s) with value v
     // (core/byzantinerandomizedconsensus.py:48-50 / :80-83 / :102-106, base/broadcast.py:30-35)
-    auto send_key = [&](uint32_t s, uint32_t v) {
+    auto send_key_now = [&](uint32_t s, uint32_t v) {
         const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint64_t m = s_meta[mbase + k];
         // a busy slot, or a phase index past this run's generation budget (brc_run): overflow
@@ -724,6 +732,28 @@ void brc_step(const Params* __restrict__ pp) {
         st_msgs += n;
         st_smax = max(st_smax, s);
         log_ev(BRC_EV_SEND, d, BRC_SEND, d * NV, s, v);
+    };
+    // During the consensus pass a replica's SENDs are queued and performed after the pass
+    // (flush_sends): a phase change reallocates the replica's own slot, while another replica may
+    // still have to count a delivery of the slot's old key from this same step -- deferring keeps
+    // every slot's metadata as the BRB phase left it for the whole pass (no snapshot needed).  The
+    // SENDs of one replica in one pass have consecutive phase indices (each phase change advances
+    // the index by one): the queue keeps the first index and a 2-bit value id per SEND.
+    bool defer_sends = false;
+    uint32_t sq_s = 0, sq_n = 0;
+    uint64_t sq_v = 0;
+    auto send_key = [&](uint32_t s, uint32_t v) {
+        if (defer_sends) {
+            if (sq_n == 0) sq_s = s;
+            if (s == sq_s + sq_n && sq_n < 32u) { sq_v |= (uint64_t)(v & 3u) << (2u * sq_n); ++sq_n; }
+            else ovf = true;                                 // cannot happen (consecutive indices, <= Q)
+            return;
+        }
+        send_key_now(s, v);
+    };
+    auto flush_sends = [&]() {
+        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (2u * i)) & 3u);
+        sq_n = 0; sq_v = 0;
     };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
@@ -766,7 +796,7 @@ void brc_step(const Params* __restrict__ pp) {
         cons_after();
     };
     auto cons_deliver = [&](uint32_t k) {
-        cons_deliver_vh((uint32_t)s_snap[mbase + k] >> 14, k >> ksh);   // snapshot (see s_snap)
+        cons_deliver_vh(m_value(s_meta[mbase + k]) & 3u, k >> ksh);    // metadata as the BRB phase left it
     };
 
     // ---- SPEC consensus (oracle spec_advance / spec_deliver): the protocol
@@ -806,8 +836,8 @@ void brc_step(const Params* __restrict__ pp) {
         }
     };
     auto spec_deliver = [&](uint32_t k) {
-        const uint32_t sn = s_snap[mbase + k];                      // snapshot (see s_snap)
-        const uint32_t s = (sn & 0x3FFFu) - 1u, v = sn >> 14, host = k >> ksh;
+        const uint64_t mk = s_meta[mbase + k];                      // as the BRB phase left it (send_key)
+        const uint32_t s = m_s1(mk) - 1u, v = m_value(mk) & 3u, host = k >> ksh;
         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
         if (s < cur) return;
         if (s >= cur + Q) { ovf = true; return; }
@@ -1029,7 +1059,7 @@ void brc_step(const Params* __restrict__ pp) {
     }
 
 #ifdef BRC_STAMPS
-    uint64_t stamp_acc[5] = {0, 0, 0, 0, 0};
+    uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t kcount[4] = {0, 0, 0, 0};
     uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
 #define BRC_STAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
@@ -1174,10 +1204,21 @@ void brc_step(const Params* __restrict__ pp) {
                 tE[i] = (lo[i] >> C32_OE_SH) & 127u; tR[i] = lo[i] >> C32_OR_SH;   // offsets: SENT ECHO / READY
             }
             BRC_KCOUNT(0);
-            // a type that cannot land on one key of the pair counts zero there: exact either way
-            const uint32_t tbu = tb[0] | tb[1];
-            if (tbu & TB_E) { ea[0] = count(tE[0]); ea[1] = count(tE[1]); }
-            if (tbu & TB_R) { ra[0] = count(tR[0]); ra[1] = count(tR[1]); }
+            // a type that cannot land on one key of the pair counts zero there: exact either way.
+            // BRC_BRANCHLESS: ECHO and READY are always evaluated (a stage without arrivals is the
+            // identity), so a pair is one basic block the scheduler can interleave
+            const uint32_t tbu = (tb[0] | tb[1]) | (BRC_BRANCHLESS ? (TB_E | TB_R) : 0u);
+            if constexpr (BRC_PERKEY_CNT) {
+                // a key's count only where its own entry has that type (the pair's stages still run
+                // for both keys: zero arrivals are the identity)
+                if (tb[0] & TB_E) ea[0] = count(tE[0]);
+                if (tb[1] & TB_E) ea[1] = count(tE[1]);
+                if (tb[0] & TB_R) ra[0] = count(tR[0]);
+                if (tb[1] & TB_R) ra[1] = count(tR[1]);
+            } else {
+                if (tbu & TB_E) { ea[0] = count(tE[0]); ea[1] = count(tE[1]); }
+                if (tbu & TB_R) { ra[0] = count(tR[0]); ra[1] = count(tR[1]); }
+            }
             if (tbu & TB_S) {
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
@@ -1215,7 +1256,7 @@ void brc_step(const Params* __restrict__ pp) {
                 ob[i] = hb & ~__ballot((lo[i] & F_DEL) != 0);
             }
             st_arr += arr2;                                      // non-honest lanes are dropped at the end
-            if (!(ob[0] | ob[1])) return;                        // no open cell receives anything now
+            if (!BRC_NOEARLY && !(ob[0] | ob[1])) return;       // no open cell receives anything now
             BRC_KCOUNT(3);
             // Per-lane work below is branch-free integer arithmetic on 0/1 flags; a stage runs only
             // when its message type can land (a stage without arrivals is the identity).
@@ -1566,48 +1607,49 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
         };
-        // lean key pipeline registers
-        uint32_t w[LCHUNK];                  // lean: compact cell words in flight
-        uint32_t kk[LCHUNK];
+        // lean key pipeline registers (LC key slots in flight: lean SPEC keeps 4, which needs no spill at 4 waves/SIMD)
+        constexpr int LC = SPEC ? BRC_LCHUNK_SPEC : LCHUNK;
+        uint32_t w[LC];                  // lean: compact cell words in flight
+        uint32_t kk[LC];
         if constexpr (LEAN) {
-            // software pipeline, unrolled by LCHUNK so the in-flight cell words never move between
+            // software pipeline, unrolled by LC so the in-flight cell words never move between
             // registers: slot c holds key p + c; right after it is processed, slot c loads key
-            // p + c + LCHUNK, so LCHUNK cell loads stay in flight.  The chunk's key metadata is read
+            // p + c + LC, so LC cell loads stay in flight.  The chunk's key metadata is read
             // at its start (a key's t_quiet update touches only its own slot, so reading ahead is
             // exact).  Slots past the list load the trash row NK and are not processed.
             auto kid = [&](uint32_t p) { return uni32(KL32 ? s_klist32[p] : (uint32_t)s_klist[p]); };
             auto cell = [&](uint32_t e) { return cld(e & TB_KEY); };
             // prologue loads pinned in slot order (the scheduler would otherwise reorder them and
             // the compiler's wait for slot 0 would then drain every load)
-            Unrolled<LCHUNK>::run([&](auto ci) {
+            Unrolled<LC>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 kk[c] = kid(c);
                 w[c] = cell(kk[c]);
                 __builtin_amdgcn_sched_barrier(0);
             });
-            for (uint32_t p = 0; p < nkeys; p += LCHUNK) {
-                uint64_t mm[LCHUNK];
-                Unrolled<LCHUNK>::run([&](auto ci) {
+            for (uint32_t p = 0; p < nkeys; p += LC) {
+                uint64_t mm[LC];
+                Unrolled<LC>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     // KL32: only the event log needs the key's metadata (phase index and value)
                     mm[c] = (EV || !KL32) ? s_meta[kk[c] & TB_KEY] : 0ull;
                 });
-                // the refill entries p + LCHUNK .. p + 2 LCHUNK - 1 in 8-B reads (p % 4 == 0 and s_klist
+                // the refill entries p + LC .. p + 2 LC - 1 in 8-B reads (p % 4 == 0 and s_klist
                 // is 8-B aligned), so a refill never waits on an LDS round trip of its own
-                static_assert(LCHUNK == 4 || LCHUNK == 8, "four or eight key-list entries per refill");
-                uint64_t knext[LCHUNK / 2];           // entries 2i | 2i + 1 << 32
-                Unrolled<LCHUNK / 4>::run([&](auto qi) {
+                static_assert(LC == 4 || LC == 8, "four or eight key-list entries per refill");
+                uint64_t knext[LC / 2];           // entries 2i | 2i + 1 << 32
+                Unrolled<LC / 4>::run([&](auto qi) {
                     constexpr int q = decltype(qi)::value;
                     if constexpr (KL32) {
-                        knext[2 * q] = *(const uint64_t*)&s_klist32[p + LCHUNK + 4 * q];
-                        knext[2 * q + 1] = *(const uint64_t*)&s_klist32[p + LCHUNK + 4 * q + 2];
+                        knext[2 * q] = *(const uint64_t*)&s_klist32[p + LC + 4 * q];
+                        knext[2 * q + 1] = *(const uint64_t*)&s_klist32[p + LC + 4 * q + 2];
                     } else {
-                        const uint64_t k4 = *(const uint64_t*)&s_klist[p + LCHUNK + 4 * q];
+                        const uint64_t k4 = *(const uint64_t*)&s_klist[p + LC + 4 * q];
                         knext[2 * q] = (k4 & 0xFFFFull) | ((k4 & 0xFFFF0000ull) << 16);
                         knext[2 * q + 1] = ((k4 >> 32) & 0xFFFFull) | ((k4 >> 48) << 32);
                     }
                 });
-                Unrolled<LCHUNK / 2>::run([&](auto ci) {
+                Unrolled<LC / 2>::run([&](auto ci) {
                     constexpr int c = 2 * decltype(ci)::value;
                     // a pair past the list is skipped; the second key of a pair at the list's end is
                     // the padding entry (the trash row, no message type): it changes nothing
@@ -1623,7 +1665,7 @@ void brc_step(const Params* __restrict__ pp) {
                     if (wr[1]) cst(kk[c + 1] & TB_KEY, nw[1]);
                     // refill (none after the last chunk: no load is left in flight past the loop, so the
                     // code after it neither waits for one nor keeps its registers)
-                    if (p + LCHUNK < nkeys) {
+                    if (p + LC < nkeys) {
                         kk[c] = uni32((uint32_t)knext[c / 2]);
                         w[c] = cell(kk[c]);
                         kk[c + 1] = uni32((uint32_t)(knext[c / 2] >> 32));
@@ -1651,6 +1693,7 @@ void brc_step(const Params* __restrict__ pp) {
                 });
             }
         }
+        BRC_STAMP(1);
         if constexpr (LEAN) {
             if (dcur != NOKEY) flush_dacc(dcur, dacc);
             // ring rows the key loop marked (every row but the current one, which it consumes), and
@@ -1667,14 +1710,11 @@ void brc_step(const Params* __restrict__ pp) {
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        BRC_STAMP(1);
+        BRC_STAMP(7);
 
-        // ================= consensus: this step's deliveries in canonical (kp, s) order
-        for (uint32_t i = lane; i < IPW * NK; i += 64) {
-            const uint64_t m = s_meta[i];
-            s_snap[i] = (uint16_t)(((m_value(m) & 3u) << 14) | (m_s1(m) & 0x3FFFu));
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // ================= consensus: this step's deliveries in canonical (kp, s) order; SENDs deferred
+        defer_sends = true;
+        BRC_STAMP(5);
         {
             const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
             const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
@@ -1697,8 +1737,8 @@ void brc_step(const Params* __restrict__ pp) {
                     const uint64_t hb = __ballot(bits != 0);
                     if (!seen_on && hb) {
                         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
-                        const uint32_t sn = s_snap[w * 64 + lane];
-                        const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;   // slot w*64+lane
+                        const uint64_t sm = s_meta[w * 64 + lane];
+                        const uint32_t ss = m_s1(sm) - 1u, sv = m_value(sm) & 3u;   // slot w*64+lane
                         const uint64_t v1 = __ballot(sv == 1), v2 = __ballot(sv == 2);
                         // one pass per distinct phase index c0 among the delivering lanes (one, or two at a
                         // phase boundary; BRC_SPEC_MULTI = 0: only words whose lanes share one index)
@@ -1738,7 +1778,7 @@ void brc_step(const Params* __restrict__ pp) {
                     // A phase change inside the word splits it: the prefix (in delivery order) that
                     // completes the phase goes at once, then the phase ends (cons_after), then the rest.
                     if (__ballot(bits != 0)) {
-                        const uint32_t sv = (uint32_t)s_snap[w * 64 + lane] >> 14;   // slot w*64+lane's value
+                        const uint32_t sv = m_value(s_meta[w * 64 + lane]) & 3u;     // slot w*64+lane's value
                         const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
                         uint32_t nb = (uint32_t)__popcll(bits);
                         const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
@@ -1800,7 +1840,7 @@ void brc_step(const Params* __restrict__ pp) {
                         uint32_t bs = 0xFFFFFFFFu;
                         for (uint64_t x = grp; x; x &= x - 1) {
                             const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                            const uint32_t s1 = s_snap[mbase + w * 64 + bb] & 0x3FFFu;
+                            const uint32_t s1 = m_s1(s_meta[mbase + w * 64 + bb]);
                             if (s1 < bs) { bs = s1; best = bb; }
                         }
                     }
@@ -1810,9 +1850,12 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
         }
-        flush_clears();                                  // keys the consensus started this step
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(2);
+        defer_sends = false;
+        flush_sends();                                   // the SENDs the consensus started this step
+        flush_clears();                                  // ... and their fresh rows
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        BRC_STAMP(6);
 
         // ================= actions stamped t
         const bool inj_mine = do_actions();
@@ -1846,8 +1889,8 @@ void brc_step(const Params* __restrict__ pp) {
     }
 
 #ifdef BRC_STAMPS
-    if (lane == 0) for (int i = 0; i < 5; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
-    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[5 + i], (unsigned long long)kcount[i]);
+    if (lane == 0) for (int i = 0; i < 8; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+    if (lane == 0) for (int i = 0; i < 4; ++i) atomicAdd(&brc_stamps[8 + i], (unsigned long long)kcount[i]);
 #endif
 #undef BRC_STAMP
     // ---- write back

@@ -23,17 +23,18 @@ else:
     _size, _per, kw = configs.workloads(L)[which]
     eng = Engine(instances=inst, **kw)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
-out = (ctypes.c_ulonglong * 9)()
+out = (ctypes.c_ulonglong * 12)()
 dbg = lib.brc_dbg_stamps16 if eng.n <= 16 else lib.brc_dbg_stamps    # each unit keeps its own timers
 eng.reset(); eng.run()
 dbg(out)
 eng.reset(); eng.run()
 dbg(out)
-tot = sum(out[:5])
-names = ["step head + key list", "key loop (BRB cells)", "consensus deliveries", "actions", "stop checks"]
-for nm, v in zip(names, out[:5]):
+tot = sum(out[:8])
+names = ["step head + key list", "key loop (BRB cells)", "consensus words", "actions", "stop checks",
+         "consensus snapshot", "consensus row clears", "key-loop tail (ring rows)"]
+for nm, v in zip(names, out[:8]):
     print("%-24s %6.1f %%  (%.3g ticks)" % (nm, 100.0 * v / tot, v))
 kn = ["key-steps processed", "  no arrivals", "  only delivered cells", "  updated"]
-for nm, v in zip(kn, out[5:]):
-    print("%-24s %.4g  (%.1f %%)" % (nm, v, 100.0 * v / max(1, out[5])))
+for nm, v in zip(kn, out[8:]):
+    print("%-24s %.4g  (%.1f %%)" % (nm, v, 100.0 * v / max(1, out[8])))
 print("kernel ms %.2f" % eng.last_kernel_ms())

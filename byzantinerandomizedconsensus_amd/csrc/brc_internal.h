@@ -49,6 +49,9 @@ constexpr int CHUNK = BRC_CHUNK;            // narrow kernel: key slots whose ce
 #endif
 constexpr int LCHUNK = BRC_LCHUNK;          // ... on the lean kernels (4 or 8; A/B round 4: 8 is 0.9 % faster)
 constexpr int KPAD = CHUNK > LCHUNK ? CHUNK : LCHUNK;   // key-list padding entries: 2 KPAD
+#ifndef BRC_KL32_SPEC
+#define BRC_KL32_SPEC 0     // lean SPEC with u32 key-list entries too (1 KB more LDS per wave at Q = 8)
+#endif
 
 struct InjDev {       // 48 B, per item CSR, sorted by t
     uint32_t t;
@@ -132,7 +135,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t h_words = cons_words(spec, msize, Q, nv);
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
-    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && !spec) ? 2u : 1u);
+    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : 1u);
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
     const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;

@@ -446,7 +446,7 @@ void brc_step(const Params* __restrict__ pp) {
     uint16_t* s_gen = (uint16_t*)(s_dbits + dbw + h_words + l_words);
     uint16_t* s_klist = s_gen + (LEAN ? 0u : ((IPW * NK + 3) & ~3u));        // this step's active key slots
     // lean REFERENCE / BEB: u32 entries (KL_*); lean SPEC keeps u16 entries (its LDS bounds its residency)
-    constexpr bool KL32 = LEAN && !SPEC;
+    constexpr bool KL32 = LEAN && (!SPEC || BRC_KL32_SPEC);
     uint32_t* s_klist32 = (uint32_t*)s_klist;
     // non-lean kernels: a window of the item's injection records, staged in LDS (INJ_CACHE at a time)
     uint64_t* s_injc = (uint64_t*)(s_klist + ((NK + 2 * KPAD + 3) & ~3u));
@@ -1099,12 +1099,11 @@ void brc_step(const Params* __restrict__ pp) {
             dwm |= 1u << wk;
         };
         uint32_t nkeys = 0;
-        for (uint32_t w = 0; w < nkw; ++w) {
-            uint64_t bits;
-            uint32_t tb = 0;                         // lean: message types that can land on slot w*64+lane
-            if constexpr (LEAN) {
-                // typed marks: ECHO / READY rows; SEND arrivals from the slot's metadata -- the SEND of
-                // slot k lands now at some receiver iff t - t_send is a delay of its sender's outset
+        if constexpr (LEAN) {
+            // typed marks: ECHO / READY rows; SEND arrivals from the slot's metadata -- the SEND of slot
+            // k lands now at some receiver iff t - t_send is a delay of its sender's outset (reading the
+            // next key word ahead measured no gain: A/B round 4)
+            for (uint32_t w = 0; w < nkw; ++w) {
                 const uint64_t mE = uni64(s_act[(row * AT + 0) * nkw + w]), mR = uni64(s_act[(row * AT + 1) * nkw + w]);
                 const uint64_t m = s_meta[w * 64 + lane];
                 const uint32_t dt = t - m_tsend(m);                        // the delay of a SEND landing now
@@ -1118,25 +1117,29 @@ void brc_step(const Params* __restrict__ pp) {
                     const uint32_t os = (uint32_t)__shfl((int)outset, (int)m_sender(m));
                     sl = m_s1(m) != 0 && dt1 < 32u && ((os >> (dt1 & 31u)) & 1u);
                 }
-                tb = (sl ? TB_S : 0u) | ((uint32_t)(mE >> lane) & 1u) * TB_E | ((uint32_t)(mR >> lane) & 1u) * TB_R;
-                bits = __ballot(tb != 0);
-            } else {
-                bits = uni64(s_act[row * nkw + w]);
-            }
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
-            if constexpr (KL32) {
-                if ((bits >> lane) & 1) {
-                    const uint64_t m = s_meta[w * 64 + lane];
-                    const uint32_t sx = (tb & TB_S) ? (((m_sender(m) & 63u) << KL_SND_SH) |
-                                                       (((t - m_tsend(m) - 1u) & 15u) << KL_DT_SH) |
-                                                       ((m & M_RESTRICTED) ? KL_RESTR : 0u)) : 0u;
-                    s_klist32[nkeys + below] = (w * 64 + lane) | (tb << TB_SH) | sx;
+                const uint32_t tb = (sl ? TB_S : 0u) | ((uint32_t)(mE >> lane) & 1u) * TB_E | ((uint32_t)(mR >> lane) & 1u) * TB_R;
+                const uint64_t bits = __ballot(tb != 0);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
+                if (tb != 0) {
+                    if constexpr (KL32) {
+                        const uint32_t sx = (tb & TB_S) ? (((m_sender(m) & 63u) << KL_SND_SH) | (((dt - 1u) & 15u) << KL_DT_SH) |
+                                                           ((m & M_RESTRICTED) ? KL_RESTR : 0u)) : 0u;
+                        s_klist32[nkeys + below] = (w * 64 + lane) | (tb << TB_SH) | sx;
+                    } else {
+                        s_klist[nkeys + below] = (uint16_t)((w * 64 + lane) | (tb << TB_SH));
+                    }
                 }
-            } else {
-                if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)((w * 64 + lane) | (tb << TB_SH));
+                nkeys += (uint32_t)__popcll(bits);
             }
-            nkeys += (uint32_t)__popcll(bits);
+        } else {
+            for (uint32_t w = 0; w < nkw; ++w) {
+                const uint64_t bits = uni64(s_act[row * nkw + w]);
+                const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bits >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bits, 0u));
+                if ((bits >> lane) & 1) s_klist[nkeys + below] = (uint16_t)(w * 64 + lane);
+                nkeys += (uint32_t)__popcll(bits);
+            }
         }
         if (lane < 2 * KPAD) {                                    // chunk padding -> the trash row
             if constexpr (KL32) s_klist32[nkeys + lane] = NK;
@@ -1698,11 +1701,13 @@ void brc_step(const Params* __restrict__ pp) {
             if (dcur != NOKEY) flush_dacc(dcur, dacc);
             // ring rows the key loop marked (every row but the current one, which it consumes), and
             // q_until = the furthest of them: the same values per-key tracking would have produced
-            const uint32_t rsh = (uint32_t)__ffs(AT * nkw) - 1u;      // AT * nkw is a power of two
             uint32_t rb = 0;
-            for (uint32_t i = lane; i < RS * AT * nkw; i += 64)
-                if (s_act[i] != 0) rb |= 1u << (i >> rsh);
-            rb = wave_or_all(rb) & ~(1u << row);
+            {
+                const uint32_t rsh = (uint32_t)__ffs(AT * nkw) - 1u;      // AT * nkw is a power of two
+                for (uint32_t i = lane; i < RS * AT * nkw; i += 64)
+                    if (s_act[i] != 0) rb |= 1u << (i >> rsh);
+                rb = wave_or_all(rb) & ~(1u << row);
+            }
             if (rb) {
                 any_rows |= rb;
                 const uint32_t rel = (row ? ((rb >> row) | (rb << (RS - row))) : rb) & (RS == 32 ? ~0u : ((1u << RS) - 1u));

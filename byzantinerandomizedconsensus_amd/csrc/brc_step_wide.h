@@ -27,6 +27,12 @@
 #pragma once
 #include "brc_step.h"
 
+#ifndef BRC_WIDE_PLANE_FENCE
+#define BRC_WIDE_PLANE_FENCE 0   // bit-plane matching: a scheduling barrier after each ballot word (A/B round 4:
+#endif                               // 59 instead of 73 spills at DM = 16, but 368 vs 338 ms on cfg5 geometric)
+#ifndef BRC_WIDE_WAVES16
+#define BRC_WIDE_WAVES16 BRC_WIDE_WAVES   // waves per SIMD the DM = 16 (geometric) instantiations allow (2: no
+#endif                                     // spills at 206 VGPRs, but 444 vs 338 ms -- occupancy wins, A/B round 4)
 #ifndef BRC_WIDE_MSTORE
 #define BRC_WIDE_MSTORE 1    // exec-masked cell stores (0: whole-row stores, unchanged words written back)
 #endif
@@ -52,7 +58,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 }
 
 template <int NPAD, int DM, bool EV, int MODE>
-__global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Params* __restrict__ pp) {
+__global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES)) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     // u64 words per cell: CONN adds the lane's ECHO and READY send-count rings (Ring16, brc_step.h)
@@ -723,14 +729,23 @@ __global__ __launch_bounds__(NPAD, BRC_WIDE_WAVES) void brc_step_wide(const Para
                     // whose counts are never used)
                     Unrolled<NW>::run([&](auto wc) {
                         constexpr int w = decltype(wc)::value;
-                        uint64_t xe = 0, xr = 0;
+                        // xe |= plane ^ PL, one 3-input bit op per plane and 32-bit half (v_bitop3 0xBE:
+                        // (a ^ b) | c); a sender matches where no plane differs
+                        uint32_t xe[2] = {0u, 0u}, xr[2] = {0u, 0u};
 #pragma unroll
                         for (int b = 0; b < NPL; ++b) {
-                            xe |= xb[b * 2 * NW + w] ^ PL[b][w];
-                            xr |= xb[b * 2 * NW + NW + w] ^ PL[b][w];
+                            const uint64_t pe = xb[b * 2 * NW + w], pr = xb[b * 2 * NW + NW + w], pl = PL[b][w];
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                xe[h] = __builtin_amdgcn_bitop3_b32((uint32_t)(pe >> (32 * h)), (uint32_t)(pl >> (32 * h)), xe[h], 0xBE);
+                                xr[h] = __builtin_amdgcn_bitop3_b32((uint32_t)(pr >> (32 * h)), (uint32_t)(pl >> (32 * h)), xr[h], 0xBE);
+                            }
                         }
-                        ea += (uint32_t)__popcll(xb[NPL * 2 * NW + w] & ~xe);
-                        ra += (uint32_t)__popcll(xb[NPL * 2 * NW + NW + w] & ~xr);
+                        const uint64_t ve = xb[NPL * 2 * NW + w], vr = xb[NPL * 2 * NW + NW + w];
+                        ea += (uint32_t)__popc((uint32_t)ve & ~xe[0]) + (uint32_t)__popc((uint32_t)(ve >> 32) & ~xe[1]);
+                        ra += (uint32_t)__popc((uint32_t)vr & ~xr[0]) + (uint32_t)__popc((uint32_t)(vr >> 32) & ~xr[1]);
+                        // one word's planes at a time: hoisting every word's LDS reads spills (DM = 16)
+                        if (BRC_WIDE_PLANE_FENCE) __builtin_amdgcn_sched_barrier(0);
                     });
                 } else if constexpr (SPARSE_D) {
                     uint32_t pwv[NW], pm = 0;

@@ -166,6 +166,8 @@ struct Engine {
     brc_event* events = nullptr; unsigned long long* event_count = nullptr;
     unsigned long long* gcount = nullptr;
     uint64_t* dbits = nullptr;                   // lean SPEC: per-wave delivery bitmaps (brc_step.h DBG)
+    uint64_t* dring = nullptr;                   // per-link lifetime kernel: delivery bitmap ring (brc_life.h)
+    bool life_pl = false;                        // lifetime kernel in its per-link delay form
     Params* dparams = nullptr;                   // device copy of the launch parameters
     Params hparams;
     std::vector<std::vector<InjDev>> pending;   // per item: uploaded-but-unconsumed + new
@@ -224,7 +226,7 @@ static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks,
 static void free_all(Engine* e) {
     void* ps[] = {e->cells, e->meta, e->mgen, e->kdst, e->act, e->actany, e->items, e->inst, e->istats,
                   e->cons0, e->cons1, e->hmask, e->inj, e->inj_off, e->inj_cnt, e->byz, e->prop, e->events,
-                  e->event_count, e->gcount, e->dbits, e->dparams};
+                  e->event_count, e->gcount, e->dbits, e->dring, e->dparams};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -411,19 +413,20 @@ int brc_create(const brc_config* cfg, void** out) {
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
                                                 c.variants, e->rs, e->compact) * WPB;
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
-    // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8,
-    // proposals from Philox or loaded, no event log, no Byzantine pattern.  BRC_KERNEL=step | life |
-    // auto (default): auto runs connection-identity peers on it (their step-kernel cells are 5 words);
-    // sender peers stay on the step kernel, which is faster there
+    // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8
+    // or per-link (uniform / geometric) delays with D <= 8, proposals from Philox or loaded, no event
+    // log, no Byzantine pattern.  BRC_KERNEL=step | life | auto (default): auto runs connection-identity
+    // peers on it (their step-kernel cells are 5 words); sender peers stay on the step kernel, which is
+    // faster there
     {
         const char* kv = getenv("BRC_KERNEL");
         const bool force_step = kv && strcmp(kv, "step") == 0, force_life = kv && strcmp(kv, "life") == 0;
         e->life_lds = lds_bytes_life(e->NK, e->nkw, spec, c.key_window, c.variants);
         const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
                               c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
-                              (c.delay_model == BRC_DELAY_CONST || c.delay_model == BRC_DELAY_SLOWSET) &&
                               c.delay_max <= 8 && e->life_lds <= 64 * 1024;
         e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION);
+        e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
     }
     // narrow kernels: one lane clears one word of a ring row (act_types words per key word)
     if ((e->wide ? e->nkw > (uint32_t)e->nkw_t : e->nkw * act_types(e->compact) > 64) || e->nitems > 0x7FFFFFFFull * WPB ||
@@ -452,6 +455,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
+        {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8 : 8},
     };
     for (auto& a : allocs)
         if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) {
@@ -466,6 +470,10 @@ int brc_create(const brc_config* cfg, void** out) {
     if (hipMemsetAsync(e->inj_off, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);
+    // the lifetime kernel leaves its bitmap ring zero at exit
+    if (e->life_cfg && e->life_pl &&
+        hipMemsetAsync(e->dring, 0, (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8, e->stream) != hipSuccess)
+        return fail(BRC_E_HIP);
     {
         std::vector<uint64_t> bm((size_t)c.instances * e->bw);
         for (uint64_t i = 0; i < c.instances; ++i)
@@ -644,6 +652,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount; P.dbits = e->dbits;
+    P.dring = e->dring;
     const uint32_t blocks = e->wide ? (uint32_t)e->nitems : (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
@@ -653,7 +662,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     e->fresh = false;
     e->last_life = life;
     if (life) {
-        rc = launch_life(kmode, (uint32_t)e->nitems, e->life_lds, e->stream, e->dparams);
+        rc = launch_life(kmode, e->life_pl, (uint32_t)e->nitems, e->life_lds, e->stream, e->dparams);
         e->life_done = true;
     } else {
         rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)

@@ -30,9 +30,19 @@
 // landing at each relative step are summed per receiver class at send time into a per-key LDS ring
 // (s_pr) instead of ballots over one send step per lane.
 //
+// Per-link delays (PL: uniform / geometric, D <= 8, SURVEY §8(d) cfg4 under cfg5's delay models).
+// Every (sender, receiver) link has its own delay, so receivers no longer fall into two classes:
+// each lane keeps the senders of each delay as a mask L[i] (bit j: link j -> lane has delay i+1,
+// drawn exactly as the step kernel draws them) and counts its arrivals at relative step r as
+// sum_i popc(ballot(sent at r - i - 1) & L[i]) -- READY copies (connection peers) through bit planes
+// of the per-lane counts kept in a 16-step byte ring.  Deliveries are no longer whole classes, so a
+// key's delivery at a future step is a bit in a per-lane HBM bitmap ring [item][RW][nkw][64]
+// (P.dring, written with no-return atomics, read and cleared by the consensus pass of that step):
+// 64 KB per instance at NK = 256 instead of the step kernel's 40-B connection cells.
+//
 // Scope (host-checked): sender- or connection-identity peers, consensus protocol with Philox or loaded
-// proposals, constant or slow-set delays with D <= 8, no injections, no event log, a fresh
-// engine run to completion.  Everything else runs on the step kernel.  Results are identical to
+// proposals, constant or slow-set delays (two-class) or uniform / geometric delays (PL) with D <= 8,
+// no injections, no event log, a fresh engine run to completion.  Everything else runs on the step kernel.  Results are identical to
 // the step kernel's (tests/test_gpu_life.py checks both against the C oracle).
 #pragma once
 #include "brc_step.h"
@@ -46,8 +56,8 @@ constexpr uint32_t LIFE_NEVER = 0xFFFFu;         // relative send step: not sent
 __device__ __forceinline__ uint32_t lm_s1(uint32_t m) { return m & 0x3FFFu; }
 __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 
-template <int MODE>
-__global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp) {
+template <int MODE, bool PL>
+__global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc_life(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     constexpr uint32_t RW = LIFE_RW;
@@ -89,9 +99,11 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
     };
 
     // ---- two delay classes: delay(j -> d) = 1 if j and d are both fast, Dd otherwise
-    uint64_t Fm = 0;                               // real fast replicas
+    uint64_t Fm = 0;                               // real fast replicas (PL: none, Dd unused)
     uint32_t Dd = P.delay_model == BRC_DELAY_CONST ? P.dconst : P.D;
-    if (P.delay_model == BRC_DELAY_SLOWSET && P.D > 1) {
+    if (PL) {
+        Dd = 1;
+    } else if (P.delay_model == BRC_DELAY_SLOWSET && P.D > 1) {
         const uint32_t off = slow_offset(P.seed, g, n);
         const bool slow = ((d + n - off) % n) < P.f;
         Fm = uni64(__ballot(real && !slow));
@@ -103,6 +115,34 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
     const uint64_t HF = Fm & hon_mask, HS = Sm & hon_mask;
     const uint32_t nHF = (uint32_t)__popcll(HF), nHS = (uint32_t)__popcll(HS);
     const bool laneF = lane_in(Fm);
+
+    // ---- PL: per-link delay masks (brc_step.h link-delay masks, NPAD = 64): L[i] = senders j whose
+    // link j -> d has delay i+1; OV[i] (wave-uniform) = senders with a delay-(i+1) link to an honest receiver
+    constexpr int DL = PL ? 8 : 1;
+    uint64_t L[DL], OV[DL];
+#pragma unroll
+    for (int i = 0; i < DL; ++i) L[i] = OV[i] = 0;
+    if constexpr (PL) {
+        if (real) {
+            for (uint32_t j4 = 0; j4 < (n + 3) / 4; ++j4) {
+                const u32x4 w = draw(P.seed, g, d, PURPOSE_DELAY, j4);
+                const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t j = 4 * j4 + q;
+                    if (j >= n) break;
+                    const uint32_t dl = (P.delay_model == BRC_DELAY_UNIFORM) ? uniform_delay(ws[q], P.D)
+                                                                             : geometric_delay(ws[q], P.D);
+#pragma unroll
+                    for (int i = 0; i < DL; ++i) if ((uint32_t)i + 1 == dl) L[i] |= 1ull << j;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < DL; ++i) OV[i] = uni64(seg_or<64, uint64_t>(honest ? L[i] : 0ull));
+    }
+    // PL: this wave's delivery-bitmap ring in HBM, word (row, w) of this lane at [(row * nkw + w) * 64]
+    uint64_t* const dring = PL ? P.dring + item * (uint64_t)RW * nkw * 64 + lane : nullptr;
 
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) { s_meta[i] = 0; s_snap[i] = 0; }
@@ -228,11 +268,21 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
         const bool oF = (Fm >> o) & 1ull;
         const uint32_t t0 = t;
         // SEND arrivals: fast receivers at 1 if the origin is fast, everyone else at Dd
-        const uint32_t sdl = (oF && laneF) ? 1u : Dd;
+        uint32_t sdl = (oF && laneF) ? 1u : Dd;
         uint64_t pendS = 0, pendE = 0, pendR = 0;     // relative steps with SEND / ECHO / READY arrivals
-        if (oF && HF) pendS |= 1ull << 1;
-        if (HS || (!oF && HF)) pendS |= 1ull << Dd;
+        if constexpr (PL) {
+            sdl = 0;
+#pragma unroll
+            for (int i = 0; i < DL; ++i) {
+                if ((L[i] >> o) & 1ull) sdl = (uint32_t)i + 1u;
+                if ((OV[i] >> o) & 1ull) pendS |= 2ull << i;
+            }
+        } else {
+            if (oF && HF) pendS |= 1ull << 1;
+            if (HS || (!oF && HF)) pendS |= 1ull << Dd;
+        }
         uint32_t fl = 0, ec = 0, rc = 0, rE = LIFE_NEVER, rR = LIFE_NEVER;
+        Ring16 ringR = {0ull, 0ull};                  // PL connection peers: READY copies per step
         uint32_t last = t0;
         if constexpr (CONN) s_pr[lane] = 0;
         const uint32_t kw = k >> 6;
@@ -242,13 +292,44 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
             const uint64_t rb = 1ull << r;
             const bool hS = (pendS & rb) != 0, hE = (pendE & rb) != 0, hR = (pendR & rb) != 0;
             pendS &= ~rb; pendE &= ~rb; pendR &= ~rb;
-            if (r > RW) { ovf = true; break; }        // cannot happen for Dd <= 8 (lifetime <= 4 Dd)
+            if (r > RW) { ovf = true; break; }        // two-class: cannot happen for Dd <= 8 (lifetime <= 4 Dd)
             const uint32_t ts = t0 + r, row = ts & (RW - 1);
             ++key_steps;
             // arrival counts per receiver class (fast: fast senders at r - 1, slow senders at r - Dd;
             // slow: every sender at r - Dd), then per lane
             const uint32_t c1 = r - 1u, cD = r >= Dd ? r - Dd : 0xFFFFFFFFu;
             uint32_t ea = 0, ra = 0, eA = 0, eB = 0, rA = 0, rB = 0;
+            if constexpr (PL) {
+                // per receiver: the senders of each delay i+1 that sent at r - i - 1
+#pragma unroll
+                for (int i = 0; i < DL; ++i) {
+                    if (!OV[i] || r <= (uint32_t)i) continue;
+                    const uint32_t sr = r - (uint32_t)i - 1u;
+                    if (hE) {
+                        const uint64_t x = __ballot(rE == sr);
+                        if (x) ea += (uint32_t)__popcll(x & L[i]);
+                    }
+                    if (hR) {
+                        if constexpr (CONN) {
+                            const uint32_t c = ring_count(ringR, rR, sr);
+                            const uint64_t x = __ballot(c != 0);
+                            if (x) {
+                                if (__ballot(c > 1u)) {
+                                    for (uint32_t b = 0; b < 8; ++b) {
+                                        const uint64_t pb = __ballot((c >> b) & 1u);
+                                        ra += (uint32_t)__popcll(pb & L[i]) << b;
+                                    }
+                                } else {
+                                    ra += (uint32_t)__popcll(x & L[i]);
+                                }
+                            }
+                        } else {
+                            const uint64_t x = __ballot(rR == sr);
+                            if (x) ra += (uint32_t)__popcll(x & L[i]);
+                        }
+                    }
+                }
+            } else {
             if (hE) {
                 const uint64_t x1 = __ballot(rE == c1), xD = __ballot(rE == cD);
                 eA = (uint32_t)__popcll(x1 & Fm) + (uint32_t)__popcll(xD & Sm);
@@ -266,12 +347,14 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
                 }
                 ra = laneF ? rA : rB;
             }
+            }
             const uint32_t sa = (hS && honest && r == sdl) ? 1u : 0u;
             const uint64_t sab = hS ? __ballot(sa != 0) : 0ull;
             const uint32_t a = ea + ra + sa;
             const uint64_t hb = __ballot(a != 0) & hon_mask;          // receivers with arrivals
             const uint32_t cells = (uint32_t)__popcll(hb);
-            const uint32_t arr = nHF * (eA + rA) + nHS * (eB + rB) + (uint32_t)__popcll(sab);
+            const uint32_t arr = PL ? wave_sum(honest ? ea + ra : 0u) + (uint32_t)__popcll(sab)
+                                    : nHF * (eA + rA) + nHS * (eB + rB) + (uint32_t)__popcll(sab);
             // a delivered cell ignores everything (core/brbroadcast.py:74)
             const bool opn = lane_in(hb) && !(fl & F_DEL);
             auto ge = [](uint32_t x, uint32_t y) -> uint32_t { return ((x - y) >> 31) ^ 1u; };   // x >= y (< 2^31)
@@ -333,6 +416,7 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
             const uint64_t eb = __ballot(es != 0), rbm = __ballot(rs != 0), db = __ballot(dl != 0);
             if (es) rE = r;
             if (!CONN && rs) rR = r;
+            if (PL && CONN && nr) { ringR = ring_put(ringR, rR, r, nr); rR = r; }
             // READY messages sent now by fast / slow senders (CONN: copies, a lane may send several)
             uint32_t cF = (uint32_t)__popcll(rbm & Fm), cS = (uint32_t)__popcll(rbm & Sm);
             if constexpr (CONN) {
@@ -347,7 +431,11 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
             }
             const uint32_t msgs = n * ((uint32_t)__popcll(eb) + cF + cS);
             const uint32_t dels = (uint32_t)__popcll(db);
-            if (db) {
+            if (PL && db) {
+                // this lane delivers the key at step ts: its bit in the lane's bitmap of row ts
+                if (dl) __hip_atomic_fetch_or(dring + (row * nkw + kw) * 64, kbit, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+            } else if (db) {
                 // receivers of one class evolve identically: a delivery step takes whole honest classes
                 const uint64_t dA = db & HF, dB = db & HS;
                 if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
@@ -356,11 +444,18 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
             }
             // the messages sent now land on fast receivers after 1 step (fast senders) and on every
             // other (sender, receiver) pair after Dd steps
-            if (eb) {
+            if (PL) {
+                // a message sent now lands after every delay i+1 some link of its sender has to an honest receiver
+#pragma unroll
+                for (int i = 0; i < DL; ++i) {
+                    if (eb & OV[i]) pendE |= rb << (i + 1);
+                    if (rbm & OV[i]) pendR |= rb << (i + 1);
+                }
+            } else if (eb) {
                 if ((eb & Fm) && HF) pendE |= rb << 1;
                 if (HS || ((eb & Sm) && HF)) pendE |= rb << Dd;
             }
-            if (rbm) {
+            if (!PL && rbm) {
                 const bool at1 = cF && HF, atD = HS || (cS && HF);
                 if (at1) pendR |= rb << 1;
                 if (atD) pendR |= rb << Dd;
@@ -429,8 +524,16 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll 1
         for (uint32_t w = 0; w < nkw; ++w) {
-            const uint64_t kA = s_dkA[row * nkw + w], kB = s_dkB[row * nkw + w];
-            uint64_t bits = cons_lane ? (laneF ? kA : kB) : 0ull;
+            uint64_t bits;
+            if constexpr (PL) {
+                uint64_t* const dp = dring + (row * nkw + w) * 64;
+                bits = __hip_atomic_load(dp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bits) __hip_atomic_store(dp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!cons_lane) bits = 0;
+            } else {
+                const uint64_t kA = s_dkA[row * nkw + w], kB = s_dkB[row * nkw + w];
+                bits = cons_lane ? (laneF ? kA : kB) : 0ull;
+            }
             if constexpr (SPEC) {
                 // word at once when every delivering lane is at one phase index c0 and its current-phase
                 // deliveries cannot complete the phase (brc_step.h, SPEC consensus pass)
@@ -524,6 +627,14 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     if (__ballot(ovf) && status != BRC_OVERFLOW) status = BRC_OVERFLOW;
+    if constexpr (PL) {
+        // rows of steps the instance did not reach: leave the bitmap ring zero for the next launch
+        for (uint32_t rm = rows; rm; rm &= rm - 1) {
+            const uint32_t row = (uint32_t)__ffs(rm) - 1u;
+            for (uint32_t w = 0; w < nkw; ++w)
+                __hip_atomic_store(dring + (row * nkw + w) * 64, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 
     // ---- write back (result readers: inst, istats, items, cons0/cons1, gcount)
     if (lane == 0) {
@@ -555,9 +666,9 @@ __global__ __launch_bounds__(64, 8) void brc_life(const Params* __restrict__ pp)
     }
 }
 
-template <int MODE>
+template <int MODE, bool PL>
 int launch_life_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_life<MODE>;
+    auto kern = brc_life<MODE, PL>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;

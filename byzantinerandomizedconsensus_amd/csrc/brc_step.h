@@ -311,7 +311,9 @@ struct Ring16 { uint64_t lo, hi; };
 constexpr uint32_t RING_MAX = 255u;
 __device__ __forceinline__ uint32_t ring_count(const Ring16& r, uint32_t tl, uint32_t s) {
     if (tl == NEVER || s > tl || tl - s >= 16u) return 0u;
-    return (uint32_t)(((s & 8u) ? r.hi : r.lo) >> (8u * (s & 7u))) & 0xFFu;
+    // half select in arithmetic form: a ?: of the two fields becomes a scratch round trip
+    const uint64_t w = r.lo ^ ((r.lo ^ r.hi) & (0ull - (uint64_t)((s >> 3) & 1u)));
+    return (uint32_t)(w >> (8u * (s & 7u))) & 0xFFu;
 }
 __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, uint32_t c) {
     if (tl == NEVER || t - tl >= 16u) {

@@ -13,7 +13,8 @@ Workloads:
   cfg2-spec, cfg3-spec   the same two in SPEC mode (the reference protocol stalls on most of them)
   cfg4-ref   2^20 instances per GPU n=64 f=21, slow-set delays D=8 (the bench.py workload)
   cfg4-spec  the same in SPEC mode (common coin, phase window 8), 2^20 instances per GPU
-  cfg4-conn  the same with connection-identity peers (what the shipped reference runs), 2^18
+  cfg4-conn  the same with connection-identity peers (what the shipped reference runs), 2^20
+  cfg4-conn-uniform[-d2]  connection peers under per-link uniform[1,4] ([1,2]) delays, 2^20
   cfg4-beb   the reference consensus over best-effort broadcast (BRC_MODE_BEB), 2^20
   cfg5-*     n=256 f=85 SPEC, 6144 instances per GPU, const / uniform[1,4] / geometric<=16
 
@@ -59,8 +60,14 @@ def workloads(L):
     }
     # cfg4 under the peer identity the shipped reference runs (core/brbroadcast.py:69: every message
     # is a new connection, no duplicate suppression; 5-word cells) and over best-effort broadcast
-    W["cfg4-conn"] = (1 << 18, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+    W["cfg4-conn"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                           round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
+    # ... and under per-link uniform delays (the lifetime kernel's per-link form): D = 4 as cfg5's
+    # uniform[1,4] (the reference protocol stalls every instance before a decision there), D = 2 (decides)
+    for dmax in (4, 2):
+        W["cfg4-conn-uniform" + ("" if dmax == 4 else "-d2")] = (
+            1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=1, delay_max=dmax, round_cap=1,
+                                key_window=4, peer_mode=L.PEER_CONNECTION))
     W["cfg4-beb"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                          round_cap=1, key_window=8, mode=L.MODE_BEB))
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
@@ -111,7 +118,8 @@ def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0, kernel="step"):
         out = {"bound": "issue", "kernel": "brc_life", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": None,
                "frac": None, "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS,
                "cell_steps_per_s": cell_steps / sec, "traffic": None, "traffic_frac": None,
-               "note": "key-lifetime kernel: cells stay in registers for a key's lifetime, no HBM cell traffic; "
+               "note": "key-lifetime kernel: cells stay in registers for a key's lifetime, no HBM cell traffic "
+                       "(per-link form: one 8-B delivery-bitmap word per lane, key word and step in HBM); "
                        "survey_model_frac prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
         t = measured_traffic(name, kernel_ms)
         if t:

@@ -188,8 +188,10 @@ int brc_read_events_range(void* engine, size_t first, brc_event* out, size_t cap
 int brc_last_kernel_ms(void* engine, float* ms);
 /* Which kernel the last brc_run launched.  BRC_KERNEL_LIFE (the key-lifetime kernel) runs a fresh
  * engine (after brc_create / brc_reset) to completion in one launch when the configuration allows:
- * n in 33..64, consensus with Philox or loaded proposals, constant or slow-set delays with
- * delay_max <= 8, no event log, no byz_pattern, no injections, max_steps == 0.  By default it runs
+ * n in 33..64, consensus with Philox or loaded proposals, delay_max <= 8 under any delay model
+ * (constant / slow-set: its two-class form; uniform / geometric: its per-link form, which keeps a
+ * 64 KB-per-instance delivery-bitmap ring in HBM at NK = 256), no event log, no byz_pattern, no
+ * injections, max_steps == 0.  By default it runs
  * connection-identity peers (BRC_PEER_CONNECTION); the environment variable BRC_KERNEL (read by
  * brc_create) = life uses it for sender peers too, = step never.  Its results equal the step
  * kernel's; its instances end final, so a later injection that would re-open a QUIESCENT instance

@@ -1,7 +1,8 @@
 """The key-lifetime kernel (csrc/brc_life.h) against the step kernel and the C oracle.
 
 The engine runs a fresh, eligible configuration (n in 33..64, consensus, constant or slow-set
-delays with D <= 8, no events, no injections; include/brc.h brc_last_kernel) on the lifetime
+delays (two-class form) or uniform / geometric delays (per-link form) with D <= 8, no events, no
+injections; include/brc.h brc_last_kernel) on the lifetime
 kernel: by default with connection-identity peers, with sender peers when BRC_KERNEL=life.  The
 step kernel is pinned to the reference fixtures (test_gpu_parity.py), so each workload here runs on
 both kernels (BRC_KERNEL=life / step at engine creation) and every output must match: per-instance status, last active
@@ -76,6 +77,23 @@ def _workloads():
                                  round_cap=2, key_window=4, byzantine=[0, 44], peer_mode=L.PEER_CONNECTION),
         "conn-slow56-r2": dict(base, n=56, f=18, seed=0xC0AC56, delay_model=L.DELAY_SLOWSET, delay_max=5, round_cap=2,
                                key_window=8, peer_mode=L.PEER_CONNECTION),
+        # per-link delays (the kernel's per-link form): uniform / geometric, every protocol mode
+        "conn-unif64": dict(base, n=64, f=21, seed=0x5EED0004, delay_model=L.DELAY_UNIFORM, delay_max=4, round_cap=1,
+                            key_window=4, peer_mode=L.PEER_CONNECTION),
+        "conn-unif64-d2-r3": dict(base, n=64, f=21, seed=0xC0DE02, delay_model=L.DELAY_UNIFORM, delay_max=2,
+                                  round_cap=3, key_window=8, peer_mode=L.PEER_CONNECTION),
+        "conn-geo64": dict(base, n=64, f=21, seed=0x6E0064, delay_model=L.DELAY_GEOMETRIC, delay_max=8, round_cap=1,
+                           key_window=4, peer_mode=L.PEER_CONNECTION),
+        "conn-unif45-byz": dict(base, n=45, f=14, seed=0xC0AD45, delay_model=L.DELAY_UNIFORM, delay_max=3, round_cap=2,
+                                key_window=8, byzantine=[1, 30], peer_mode=L.PEER_CONNECTION),
+        "ref-unif64-d2-r3": dict(base, n=64, f=21, seed=0x5EED0044, delay_model=L.DELAY_UNIFORM, delay_max=2,
+                                 round_cap=3, key_window=8),
+        "ref-geo64-cap30": dict(base, n=64, f=21, seed=0x5EED0054, delay_model=L.DELAY_GEOMETRIC, delay_max=6,
+                                round_cap=0, key_window=32, step_cap=30),
+        "spec-unif64": dict(base, n=64, f=21, seed=0x5EED0064, delay_model=L.DELAY_UNIFORM, delay_max=4, round_cap=2,
+                            key_window=8, mode=L.MODE_SPEC, coin_seed=COIN),
+        "beb-geo48": dict(base, n=48, f=15, seed=0x5EED0074, delay_model=L.DELAY_GEOMETRIC, delay_max=5, round_cap=1,
+                          key_window=8, mode=L.MODE_BEB),
         "ref-loaded-slow48": dict(base, n=48, f=15, seed=0x4803, delay_model=L.DELAY_SLOWSET, delay_max=6, round_cap=1,
                                   key_window=4, proposals=L.PROPOSALS_LOADED),
     }
@@ -166,7 +184,7 @@ def test_lifetime_kernel_equals_step_kernel_and_oracle(name):
 
 def test_kernel_choice():
     """Default choice: connection peers run on the lifetime kernel, sender peers on the step kernel
-    (faster there); event logs, injections, stepped runs and random delays stay on the step kernel;
+    (faster there); event logs, injections, stepped runs and delays past 8 stay on the step kernel;
     a lifetime-run instance cannot be re-opened by an injection."""
     from byzantinerandomizedconsensus_amd.engine import Engine
     L = _L()
@@ -187,7 +205,10 @@ def test_kernel_choice():
         assert eng.last_kernel() == "step"
     with Engine(instances=4, **dict(kw, delay_model=L.DELAY_UNIFORM, delay_max=4)) as eng:
         eng.run()
-        assert eng.last_kernel() == "step"
+        assert eng.last_kernel() == "life"                # per-link form
+    with Engine(instances=4, **dict(kw, delay_model=L.DELAY_GEOMETRIC, delay_max=16)) as eng:
+        eng.run()
+        assert eng.last_kernel() == "step"                # D > 8
     with Engine(instances=4, **kw) as eng:
         eng.inject([dict(t=0, kind=L.INJ_PROPOSE, instance=0, node=0, value=1)])
         eng.run()
@@ -202,3 +223,23 @@ def test_kernel_choice():
         if eng.instances_result(0, 1)[0]["status"] == "quiescent":
             with pytest.raises(L.EngineError):
                 eng.inject([dict(t=30, kind=L.INJ_PROPOSE, instance=0, node=0, value=1)])
+
+
+def test_per_link_rerun_after_reset():
+    """The per-link form leaves its HBM delivery-bitmap ring zero (rows of steps a stopped instance
+    never reached are cleared at exit): a reset engine's second lifetime run equals its first."""
+    from byzantinerandomizedconsensus_amd.engine import Engine
+    kw = _workloads()["ref-geo64-cap30"]
+    os.environ["BRC_KERNEL"] = "life"
+    try:
+        eng = Engine(instances=512, **kw)
+    finally:
+        os.environ.pop("BRC_KERNEL", None)
+    with eng:
+        eng.run()
+        a = (eng.instances_result(), eng.replicas())
+        eng.reset()
+        eng.run()
+        assert eng.last_kernel() == "life"
+        b = (eng.instances_result(), eng.replicas())
+    assert a == b

@@ -32,7 +32,7 @@ KERNEL_STEP, KERNEL_LIFE = 0, 1
 
 EXPORTS = ["brc_create", "brc_load_proposals", "brc_load_byzantine", "brc_inject", "brc_run",
            "brc_reset", "brc_read_instances", "brc_read_replicas", "brc_read_events",
-           "brc_read_stats", "brc_read_round_histogram", "brc_read_decisions", "brc_reset_at",
+           "brc_read_stats", "brc_read_round_histogram", "brc_read_decisions", "brc_read_value_decisions", "brc_reset_at",
            "brc_read_events_range", "brc_last_kernel_ms", "brc_last_kernel", "brc_device_count", "brc_last_error",
            "brc_destroy", "brc_abi_version"]
 
@@ -123,6 +123,7 @@ def load():
         "brc_read_stats": ([vp, ctypes.POINTER(Stats)], ctypes.c_int),
         "brc_read_round_histogram": ([vp, ctypes.c_void_p, ctypes.c_uint32], ctypes.c_int),
         "brc_read_decisions": ([vp, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
+        "brc_read_value_decisions": ([vp, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)], ctypes.c_int),
         "brc_reset_at": ([vp, ctypes.c_uint64], ctypes.c_int),
         "brc_read_events_range": ([vp, ctypes.c_size_t, ctypes.POINTER(Event), ctypes.c_size_t,
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),

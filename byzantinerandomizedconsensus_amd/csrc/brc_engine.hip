@@ -102,33 +102,33 @@ __global__ void round_histogram(const uint64_t* cons1, const uint64_t* byz, uint
         if (sh[b]) atomicAdd(&hist[b], sh[b]);
 }
 
-// First decisions of the honest replicas (brc_read_decisions): per instance, count each honest
-// replica's first decided value id (bin 4: never decided) and flag instances whose honest replicas
+// First decisions of the honest replicas (brc_read_value_decisions): per instance, count each honest
+// replica's first decided value id (bin 8: never decided) and flag instances whose honest replicas
 // decided different values.  One thread per instance; bins reduced in LDS first.
 __global__ void decision_histogram(const uint64_t* cons1, const uint64_t* byz, uint64_t instances, uint32_t ipw,
                                    uint32_t lpi, uint32_t npad, uint32_t bw, uint32_t n,
-                                   unsigned long long* out /* [6]: 5 value bins, disagreements */) {
-    __shared__ unsigned long long sh[6];
-    if (threadIdx.x < 6) sh[threadIdx.x] = 0;
+                                   unsigned long long* out /* [10]: 9 value bins, disagreements */) {
+    __shared__ unsigned long long sh[10];
+    if (threadIdx.x < 10) sh[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t in = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (in < instances) {
         const uint64_t item = in / ipw, seg = in % ipw;
-        uint32_t cnt[5] = {0, 0, 0, 0, 0};
+        uint32_t cnt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         uint32_t seen = 0;                       // value ids decided by some honest replica
         for (uint32_t d = 0; d < n; ++d) {
             if ((byz[in * bw + d / 64] >> (d % 64)) & 1ull) continue;
             const uint64_t c1 = cons1[item * lpi + seg * npad + d];
-            if ((c1 & 0xFFFF) == 0) { ++cnt[4]; continue; }
-            const uint32_t v = (uint32_t)(c1 >> 48) & 3u;      // first decided value id
+            if ((c1 & 0xFFFF) == 0) { ++cnt[8]; continue; }
+            const uint32_t v = (uint32_t)(c1 >> 48) & 7u;      // first decided value id
             ++cnt[v];
             seen |= 1u << v;
         }
-        for (int b = 0; b < 5; ++b) if (cnt[b]) atomicAdd(&sh[b], (unsigned long long)cnt[b]);
-        if (seen & (seen - 1)) atomicAdd(&sh[5], 1ull);
+        for (int b = 0; b < 9; ++b) if (cnt[b]) atomicAdd(&sh[b], (unsigned long long)cnt[b]);
+        if (seen & (seen - 1)) atomicAdd(&sh[9], 1ull);
     }
     __syncthreads();
-    if (threadIdx.x < 6 && sh[threadIdx.x]) atomicAdd(&out[threadIdx.x], sh[threadIdx.x]);
+    if (threadIdx.x < 10 && sh[threadIdx.x]) atomicAdd(&out[threadIdx.x], sh[threadIdx.x]);
 }
 
 // grid-stride fill: a dispatch holds < 2^32 work-items per dimension, and the cell array can
@@ -168,6 +168,8 @@ struct Engine {
     uint64_t* dbits = nullptr;                   // lean SPEC: per-wave delivery bitmaps (brc_step.h DBG)
     uint64_t* dring = nullptr;                   // per-link lifetime kernel: delivery bitmap ring (brc_life.h)
     bool life_pl = false;                        // lifetime kernel in its per-link delay form
+    uint32_t nval = 4;                           // consensus value ids the step kernel keeps (value_ids)
+    bool values_wide = false;                    // a loaded proposal uses a value id >= 4 (no lifetime kernel)
     Params* dparams = nullptr;                   // device copy of the launch parameters
     Params hparams;
     std::vector<std::vector<InjDev>> pending;   // per item: uploaded-but-unconsumed + new
@@ -412,7 +414,8 @@ int brc_create(const brc_config* cfg, void** out) {
                                             spec, c.key_window)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
                                                 c.variants, e->rs, e->compact) * WPB;
-    e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants);
+    e->nval = value_ids(!e->compact && !e->wide);
+    e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants, e->nval);
     // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8
     // or per-link (uniform / geometric) delays with D <= 8, proposals from Philox or loaded, no event
     // log, no Byzantine pattern.  BRC_KERNEL=step | life | auto (default): auto runs connection-identity
@@ -494,8 +497,16 @@ int brc_load_proposals(void* h, const int8_t* proposals) {
     if (!e || !proposals) return BRC_E_INVALID;
     if (e->cfg.proposals != BRC_PROPOSALS_LOADED) return BRC_E_STATE;
     const size_t bytes = e->cfg.instances * e->cfg.n;
-    for (size_t i = 0; i < bytes; ++i)
-        if (proposals[i] < 0 || proposals[i] > 3) { e->err = "proposal value ids must be in [0, 3]"; return BRC_E_INVALID; }
+    const int vmax = e->cfg.mode == BRC_MODE_SPEC ? 3 : (int)e->nval - 1;
+    bool wide_ids = false;
+    for (size_t i = 0; i < bytes; ++i) {
+        if (proposals[i] < 0 || proposals[i] > vmax) {
+            e->err = "proposal value ids must be in [0, " + std::to_string(vmax) + "] on this kernel";
+            return BRC_E_INVALID;
+        }
+        wide_ids = wide_ids || proposals[i] > 3;
+    }
+    e->values_wide = wide_ids;               // the lifetime kernel keeps 2-bit value ids
     if (!e->prop) HIPCHK(e, hipMalloc(&e->prop, bytes));
     HIPCHK(e, hipMemcpyAsync(e->prop, proposals, bytes, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -532,7 +543,10 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
     for (size_t i = 0; i < count; ++i) {
         const brc_injection& x = list[i];
         if (x.instance >= c.instances || x.node >= c.n || x.t > c.step_cap) { e->err = "injection out of range"; return BRC_E_INVALID; }
-        if (x.value < 0 || x.value > 3 || x.s >= 0xFFFE) { e->err = "value id / phase index out of range"; return BRC_E_INVALID; }
+        if (x.value < 0 || x.value >= (int)(c.mode == BRC_MODE_SPEC ? 4u : e->nval) || x.s >= 0xFFFE) {
+            e->err = "value id / phase index out of range (value ids 4..7 need n <= 32 or connection peers, not SPEC)";
+            return BRC_E_INVALID;
+        }
         InjDev r = {};
         r.t = x.t; r.kind = (uint8_t)x.kind; r.type = (uint8_t)x.type; r.node = (uint8_t)x.node;
         r.seg = (uint8_t)(x.instance % e->ipw); r.value = (int8_t)x.value; r.s = (uint16_t)x.s;
@@ -623,7 +637,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     if (rc) return rc;
     bool no_inj = true;
     for (const auto& v : e->pending) if (!v.empty()) { no_inj = false; break; }
-    const bool life = e->life_cfg && e->fresh && no_inj && max_steps == 0;
+    const bool life = e->life_cfg && e->fresh && no_inj && max_steps == 0 && !e->values_wide;
     if (!life) {
         rc = ensure_cells(e);
         if (rc) return rc;
@@ -756,7 +770,7 @@ int brc_read_replicas(void* h, uint64_t first, uint64_t count, brc_replica_resul
             const size_t l = (item - i0) * e->lpi + seg * e->npad + dd;
             brc_replica_result& r = out[i * e->cfg.n + dd];
             const uint64_t a = c0[l], b = c1[l];
-            r.round = a & 0xFFFF; r.phase = (a >> 16) & 0xFF; r.value_count = (a >> 48) & 0xFFFF;
+            r.round = a & 0xFFFF; r.phase = (a >> 16) & 0xF; r.value_count = (a >> 48) & 0xFFFF;   // cons0_pack
             r.decide_count = b & 0xFFFF; r.first_decide_round = (b >> 16) & 0xFFFF;
             r.first_decide_t = (b >> 32) & 0xFFFF;
             r.first_decide_value = r.decide_count ? (int32_t)((b >> 48) & 0xFF) : -1;
@@ -841,14 +855,14 @@ int brc_read_round_histogram(void* h, uint64_t* hist, uint32_t bins) {
     return BRC_OK;
 }
 
-int brc_read_decisions(void* h, uint64_t* value_hist, uint64_t* disagreements) {
+int brc_read_value_decisions(void* h, uint64_t* value_hist, uint64_t* disagreements) {
     Engine* e = static_cast<Engine*>(h);
     if (!e || !value_hist || !disagreements) return BRC_E_INVALID;
     if (e->cfg.protocol != BRC_PROTO_CONSENSUS) { e->err = "decisions need the consensus protocol"; return BRC_E_STATE; }
     HIPCHK(e, hipSetDevice(e->cfg.device));
     unsigned long long* d = nullptr;
-    HIPCHK(e, hipMalloc(&d, 6 * 8));
-    hipError_t r = hipMemsetAsync(d, 0, 6 * 8, e->stream);
+    HIPCHK(e, hipMalloc(&d, 10 * 8));
+    hipError_t r = hipMemsetAsync(d, 0, 10 * 8, e->stream);
     if (r == hipSuccess) {
         const uint32_t tpb = 256;
         const uint32_t blocks = (uint32_t)((e->cfg.instances + tpb - 1) / tpb);
@@ -856,13 +870,26 @@ int brc_read_decisions(void* h, uint64_t* value_hist, uint64_t* disagreements) {
                            e->cfg.instances, (uint32_t)e->ipw, e->lpi, (uint32_t)e->npad, e->bw, e->cfg.n, d);
         r = hipGetLastError();
     }
-    unsigned long long hout[6] = {0};
+    unsigned long long hout[10] = {0};
     if (r == hipSuccess) r = hipMemcpyAsync(hout, d, sizeof(hout), hipMemcpyDeviceToHost, e->stream);
     if (r == hipSuccess) r = hipStreamSynchronize(e->stream);
     (void)hipFree(d);
     if (r != hipSuccess) { e->err = std::string("decision histogram: ") + hipGetErrorString(r); return BRC_E_HIP; }
-    for (int b = 0; b < 5; ++b) value_hist[b] = hout[b];
-    *disagreements = hout[5];
+    for (int b = 0; b < 9; ++b) value_hist[b] = hout[b];
+    *disagreements = hout[9];
+    return BRC_OK;
+}
+
+int brc_read_decisions(void* h, uint64_t* value_hist, uint64_t* disagreements) {
+    Engine* e = static_cast<Engine*>(h);
+    if (!e || !value_hist || !disagreements) return BRC_E_INVALID;
+    uint64_t v9[9];
+    const int rc = brc_read_value_decisions(h, v9, disagreements);
+    if (rc) return rc;
+    for (int b = 4; b < 8; ++b)
+        if (v9[b]) { e->err = "value ids >= 4 were decided: use brc_read_value_decisions"; return BRC_E_STATE; }
+    for (int b = 0; b < 4; ++b) value_hist[b] = v9[b];
+    value_hist[4] = v9[8];
     return BRC_OK;
 }
 

@@ -109,11 +109,24 @@ __host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) 
     return model == BRC_DELAY_CONST ? 1u : model == BRC_DELAY_SLOWSET ? (dmax > 1 ? 2u : 1u) : dmax;
 }
 
-// u64 words of a wave's consensus LDS area: REFERENCE hm[4][64] T; SPEC [seen[Q][64] T +] cnt[Q][64] u32
-__host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32_t Q, uint32_t nv) {
+// Consensus value ids (core/byzantinerandomizedconsensus.py:57-60 keys its tables by payload string;
+// id 0 is str(NONE) == "-1"): 2 bits (3 strings + "-1") on the lean, wide and key-lifetime kernels,
+// 3 bits (7 strings + "-1") on the other narrow kernels (NPAD <= 32, and connection peers).
+__host__ __device__ constexpr uint32_t value_ids(bool narrow_full) { return narrow_full ? 8u : 4u; }
+
+// Consensus record word 0 (cons0): round [0,16) | phase [16,20) | nvals [20,24) | order [24,48) (the
+// value ids in insertion order, 2 or 3 bits each) | value_count [48,64)
+__host__ __device__ inline uint64_t cons0_pack(uint32_t round, uint32_t phase, uint32_t nvals, uint32_t order,
+                                               uint32_t vcount) {
+    return (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xF) << 16) | ((uint64_t)(nvals & 0xF) << 20) |
+           ((uint64_t)(order & 0xFFFFFF) << 24) | ((uint64_t)(vcount & 0xFFFF) << 48);
+}
+
+// u64 words of a wave's consensus LDS area: REFERENCE hm[nval][64] T; SPEC [seen[Q][64] T +] cnt[Q][64] u32
+__host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32_t Q, uint32_t nv, uint32_t nval = 4) {
     // SPEC with one key variant per origin: a replica delivers each (origin, phase) key at most
     // once, so the origin count needs no host set (seen masks only when nv > 1)
-    return spec ? (Q * 64 * (nv > 1 ? msize : 0u) + Q * 64 * 4 + 7) / 8 : (4 * 64 * msize + 7) / 8;
+    return spec ? (Q * 64 * (nv > 1 ? msize : 0u) + Q * 64 * 4 + 7) / 8 : (nval * 64 * msize + 7) / 8;
 }
 
 // Activity-ring words per (row, key word): the lean kernels keep one ECHO and one READY row (typed
@@ -133,7 +146,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
                                                        uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
     const uint32_t ipw = 64 / (uint32_t)npad;
     const uint32_t msize = npad <= 8 ? 1 : (uint32_t)npad / 8;
-    const uint32_t h_words = cons_words(spec, msize, Q, nv);
+    const uint32_t h_words = cons_words(spec, msize, Q, nv, value_ids(!lean));
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
     const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : 1u);
@@ -174,8 +187,9 @@ __host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32
 
 // Bytes of the global consensus-set buffer (hmask) per item: REFERENCE host masks [4][lanes] of
 // n bits; SPEC phase windows seen[Q][lanes] (n bits; narrow kernel only) + cnt[Q][lanes] u32.
-inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32_t msize, uint32_t Q, uint32_t nv) {
-    return spec ? (uint64_t)Q * lanes * ((wide || nv == 1 ? 0 : msize) + 4) : 4ull * lanes * msize;
+inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32_t msize, uint32_t Q, uint32_t nv,
+                                    uint32_t nval = 4) {
+    return spec ? (uint64_t)Q * lanes * ((wide || nv == 1 ? 0 : msize) + 4) : (uint64_t)nval * lanes * msize;
 }
 
 // Key-lifetime kernel (brc_life.h): ring steps (> 4 Dd - 1 for Dd <= 8) and LDS bytes of one wave

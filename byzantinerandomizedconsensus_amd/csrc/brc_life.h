@@ -650,8 +650,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
     }
     const size_t li = item * 64 + lane;
     if (honest) {
-        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
-                          ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        gp(P.cons0)[li] = cons0_pack(round, phase, nvals, order, vcount);
         gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                           ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
     }

@@ -415,6 +415,10 @@ void brc_step(const Params* __restrict__ pp) {
     constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
     constexpr int IPW = 64 / NPAD;
     constexpr uint32_t AT = act_types(LEAN);     // activity-ring words per (row, key word)
+    // consensus value ids (brc_internal.h value_ids): VB bits each, NVAL of them; VREP has a 1 in
+    // the low bit of every VB-bit field of `order`
+    constexpr uint32_t NVAL = value_ids(!LEAN), VB = LEAN ? 2u : 3u, VMASK = NVAL - 1u;
+    constexpr uint32_t VREP = LEAN ? 0x55u : 0x249249u;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
     // wid via readfirstlane: the item (and every address derived from it) is then provably wave-uniform
@@ -427,9 +431,9 @@ void brc_step(const Params* __restrict__ pp) {
     const uint32_t qsh = (uint32_t)__ffs(Q) - 1u, Qm = Q - 1u, ksh = qsh + (uint32_t)__ffs(NV) - 1u;
     // per-wave LDS carve (lds_bytes_per_wave): meta[IPW*NK] u64 | act[TS][nkw] u64 |
     //     dbits[nkw][64] u64 | consensus area | L[nL][64] T | mgen[IPW*NK] u16 | klist[NK + 2 CHUNK] u16
-    // consensus area: REFERENCE hm[4][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
+    // consensus area: REFERENCE hm[NVAL][64] T;  SPEC seen[Q][64] T, cnt[Q][64] u32
     const uint32_t nL = NLR ? 0u : P.nL;        // NLR: the masks live in registers, not in LDS
-    const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV);
+    const uint32_t h_words = cons_words(SPEC, (uint32_t)sizeof(T), Q, NV, NVAL);
     const bool seen_on = NV > 1;                 // SPEC: host sets needed only with key variants
     const uint32_t l_words = (nL * 64 * (uint32_t)sizeof(T) + 7) / 8;
     uint64_t* s_meta = smem + (size_t)wid * (lds_bytes_per_wave(NPAD, NK, nkw, nL, SPEC, Q, NV, RS, LEAN) / 8);
@@ -671,10 +675,11 @@ void brc_step(const Params* __restrict__ pp) {
             s_cnt[q * 64 + lane] = cons_lane ? gp(gcnt)[(item * Q + q) * 64 + lane] : 0u;
         }
     } else {
-        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = cons_lane ? gp((const T*)P.hmask)[(item * 4 + v) * 64 + lane] : (T)0;
+        for (uint32_t v = 0; v < NVAL; ++v)
+            s_hm[v * 64 + lane] = cons_lane ? gp((const T*)P.hmask)[(item * NVAL + v) * 64 + lane] : (T)0;
     }
-    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
-    uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
+    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xF, nvals = (c0 >> 20) & 0xF;   // cons0_pack
+    uint32_t order = (c0 >> 24) & 0xFFFFFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
     uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
 
@@ -740,33 +745,33 @@ void brc_step(const Params* __restrict__ pp) {
     // still have to count a delivery of the slot's old key from this same step -- deferring keeps
     // every slot's metadata as the BRB phase left it for the whole pass (no snapshot needed).  The
     // SENDs of one replica in one pass have consecutive phase indices (each phase change advances
-    // the index by one): the queue keeps the first index and a 2-bit value id per SEND.
+    // the index by one): the queue keeps the first index and a VB-bit value id per SEND.
     bool defer_sends = false;
     uint32_t sq_s = 0, sq_n = 0;
     uint64_t sq_v = 0;
     auto send_key = [&](uint32_t s, uint32_t v) {
         if (defer_sends) {
             if (sq_n == 0) sq_s = s;
-            if (s == sq_s + sq_n && sq_n < 32u) { sq_v |= (uint64_t)(v & 3u) << (2u * sq_n); ++sq_n; }
+            if (s == sq_s + sq_n && sq_n < 64u / VB) { sq_v |= (uint64_t)(v & VMASK) << (VB * sq_n); ++sq_n; }
             else ovf = true;                                 // cannot happen (consecutive indices, <= Q)
             return;
         }
         send_key_now(s, v);
     };
     auto flush_sends = [&]() {
-        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (2u * i)) & 3u);
+        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (VB * i)) & VMASK);
         sq_n = 0; sq_v = 0;
     };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
-            const uint32_t v = (order >> (2 * i)) & 3;
+            const uint32_t v = (order >> (VB * i)) & VMASK;
             if (2 * popc(s_hm[v * 64 + lane]) > bound2) return v;
         }
         return 0;                                                    // str(NONE) == "-1"
     };
     auto cons_reset = [&]() {
         vcount = 0; nvals = 0; order = 0;
-        for (int v = 0; v < 4; ++v) s_hm[v * 64 + lane] = 0;
+        for (uint32_t v = 0; v < NVAL; ++v) s_hm[v * 64 + lane] = 0;
     };
     // :71-106: the phase ends a delivery may complete (value_count has just grown)
     auto cons_after = [&]() {
@@ -788,17 +793,17 @@ void brc_step(const Params* __restrict__ pp) {
     };
     // :53-106 for a message of `host` carrying value id v (a BRB delivery, or BRC_INJ_DELIVER)
     auto cons_deliver_vh = [&](uint32_t v, uint32_t host) {
-        // v already inserted? compare it with every 2-bit field of `order` at once (nvals <= 4)
-        const uint32_t x = order ^ (v * 0x55u);                      // a field is 0 where it equals v
-        const uint32_t valid = (1u << (2 * nvals)) - 1u;              // fields in use
-        const bool found = (~(x | (x >> 1)) & 0x55u & valid) != 0;
-        if (!found) { order |= v << (2 * nvals); ++nvals; }         // :57-58
+        // v already inserted? compare it with every VB-bit field of `order` at once (nvals <= NVAL)
+        const uint32_t x = order ^ (v * VREP);                       // a field is 0 where it equals v
+        const uint32_t valid = (1u << (VB * nvals)) - 1u;             // fields in use
+        const bool found = (~(x | (x >> 1) | (VB == 3 ? x >> 2 : 0u)) & VREP & valid) != 0;
+        if (!found) { order |= v << (VB * nvals); ++nvals; }        // :57-58
         s_hm[v * 64 + lane] |= (T)((T)1 << host);                   // :60
         ++vcount;                                                    // :61
         cons_after();
     };
     auto cons_deliver = [&](uint32_t k) {
-        cons_deliver_vh(m_value(s_meta[mbase + k]) & 3u, k >> ksh);    // metadata as the BRB phase left it
+        cons_deliver_vh(m_value(s_meta[mbase + k]) & VMASK, k >> ksh); // metadata as the BRB phase left it
     };
 
     // ---- SPEC consensus (oracle spec_advance / spec_deliver): the protocol
@@ -934,7 +939,7 @@ void brc_step(const Params* __restrict__ pp) {
                 const uint32_t v = (P.proposals == BRC_PROPOSALS_PHILOX) ? proposal_id(P.seed, g, d)
                                                                          : (uint32_t)gp(P.prop)[inst * n + d];
                 round = 1; phase = 1;                                 // :43-47
-                send_key(0, v & 3);
+                send_key(0, v & (SPEC ? 3u : VMASK));
                 if constexpr (SPEC) spec_advance();                   // phase 0 may be buffered
             }
             flush_clears();
@@ -947,13 +952,13 @@ void brc_step(const Params* __restrict__ pp) {
             mine_any |= mine;
             if (r.kind == BRC_INJ_PROPOSE) {
                 if (mine && honest && d == r.node) {
-                    round = 1; phase = 1; send_key(0, (uint32_t)r.value & 3);
+                    round = 1; phase = 1; send_key(0, (uint32_t)r.value & (SPEC ? 3u : VMASK));
                     if constexpr (SPEC) spec_advance();
                 }
             } else if (r.kind == BRC_INJ_DELIVER) {
                 // a direct deliver() call (brc_inject refuses it for SPEC): host in r.slot
                 if constexpr (!SPEC) {
-                    if (mine && honest && d == r.node) cons_deliver_vh((uint32_t)r.value & 3, r.slot);
+                    if (mine && honest && d == r.node) cons_deliver_vh((uint32_t)r.value & VMASK, r.slot);
                 }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the
@@ -1917,8 +1922,7 @@ void brc_step(const Params* __restrict__ pp) {
         P.items[item] = o;
     }
     if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
-        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
-                      ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        gp(P.cons0)[li] = cons0_pack(round, phase, nvals, order, vcount);
         gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                       ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
         if constexpr (SPEC) {
@@ -1929,7 +1933,7 @@ void brc_step(const Params* __restrict__ pp) {
                 gp(gcnt)[(item * Q + q) * 64 + lane] = s_cnt[q * 64 + lane];
             }
         } else {
-            for (int v = 0; v < 4; ++v) gp((T*)P.hmask)[(item * 4 + v) * 64 + lane] = s_hm[v * 64 + lane];
+            for (uint32_t v = 0; v < NVAL; ++v) gp((T*)P.hmask)[(item * NVAL + v) * 64 + lane] = s_hm[v * 64 + lane];
         }
     }
     if (LEAN && lane != 0) { st_cells = 0; st_del = 0; st_bcast = 0; }   // lean: wave-uniform counts

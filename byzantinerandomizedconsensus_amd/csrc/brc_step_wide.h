@@ -259,8 +259,8 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
             for (uint32_t w = 0; w < NW; ++w)
                 hm(v, w) = cons_lane ? gp((const uint64_t*)P.hmask)[((inst * 4 + v) * NW + w) * NPAD + d] : 0ull;
     }
-    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xFF, nvals = (c0 >> 24) & 0xFF;
-    uint32_t order = (c0 >> 32) & 0xFF, vcount = (c0 >> 48) & 0xFFFF;
+    uint32_t round = c0 & 0xFFFF, phase = (c0 >> 16) & 0xF, nvals = (c0 >> 20) & 0xF;   // cons0_pack
+    uint32_t order = (c0 >> 24) & 0xFFFFFF, vcount = (c0 >> 48) & 0xFFFF;
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
     uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
 
@@ -943,8 +943,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
         P.items[inst] = o;
     }
     if (honest && P.protocol == BRC_PROTO_CONSENSUS) {
-        gp(P.cons0)[li] = (uint64_t)(round & 0xFFFF) | ((uint64_t)(phase & 0xFF) << 16) | ((uint64_t)(nvals & 0xFF) << 24) |
-                          ((uint64_t)(order & 0xFF) << 32) | ((uint64_t)(vcount & 0xFFFF) << 48);
+        gp(P.cons0)[li] = cons0_pack(round, phase, nvals, order, vcount);
         gp(P.cons1)[li] = (uint64_t)(dcount & 0xFFFF) | ((uint64_t)(frnd & 0xFFFF) << 16) | ((uint64_t)(ft & 0xFFFF) << 32) |
                           ((uint64_t)(fval & 0xFF) << 48) | ((uint64_t)(lval & 0xFF) << 56);
         if constexpr (SPEC) {

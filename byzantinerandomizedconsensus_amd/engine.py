@@ -174,16 +174,22 @@ class Engine:
         return [(e.instance, e.t, e.kind, e.node, e.type, e.a, e.b, e.value) for e in arr[:cap]], total.value
 
     def decisions(self, labels=("-1", "0", "1", "3")):
-        """First decisions of the honest replicas: ({label of value id 0..3: c, "undecided": c},
-        instances whose honest replicas decided different values).  The default labels are the
-        wire codec's value table (Philox proposals); pass the strings your value ids stand for
-        (e.g. a Cluster's value table) to label loaded proposals."""
-        if len(labels) != 4 or len(set(labels)) != 4 or "undecided" in labels:
-            raise ValueError("labels: four distinct value strings, not 'undecided'")
-        arr = np.zeros(5, dtype=np.uint64)
+        """First decisions of the honest replicas: ({label of value id v: c, "undecided": c},
+        instances whose honest replicas decided different values).  labels[v] is the string value
+        id v stands for (1 to 8 of them; id 0 is "-1").  The default labels are the wire codec's
+        value table (Philox proposals); pass the strings your value ids stand for (e.g. a
+        Cluster's value table) to label loaded proposals.  A decided id past the labels raises."""
+        labels = tuple(labels)
+        if not 1 <= len(labels) <= 8 or len(set(labels)) != len(labels) or "undecided" in labels:
+            raise ValueError("labels: 1 to 8 distinct value strings, not 'undecided'")
+        arr = np.zeros(9, dtype=np.uint64)
         dis = ctypes.c_uint64(0)
-        self._chk(self._lib.brc_read_decisions(self._h, arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(dis)))
-        return dict(zip(tuple(labels) + ("undecided",), (int(x) for x in arr))), dis.value
+        self._chk(self._lib.brc_read_value_decisions(self._h, arr.ctypes.data_as(ctypes.c_void_p), ctypes.byref(dis)))
+        if any(int(x) for x in arr[len(labels):8]):
+            raise ValueError("value ids past the %d labels were decided: %s" % (len(labels), [int(x) for x in arr[:8]]))
+        out = {labels[v]: int(arr[v]) for v in range(len(labels))}
+        out["undecided"] = int(arr[8])
+        return out, dis.value
 
     def round_histogram(self, bins=66):
         """hist[r] = instances whose honest replicas had all decided by round r; hist[0] =

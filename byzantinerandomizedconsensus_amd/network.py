@@ -21,7 +21,9 @@ Deviations from the reference, all reported by exceptions and never silent:
 * Consensus has no stop in the reference (it re-proposes forever,
   ``core/byzantinerandomizedconsensus.py:102-106``).  Clusters stop once every node has
   decided ``round_cap`` times (``configure``).
-* At most three distinct proposal strings besides ``"-1"`` (two-bit value ids).
+* At most seven distinct proposal strings besides ``"-1"`` (three-bit value ids) -- three on
+  clusters of 33..64 nodes with ``peer_mode="sender"`` and above 64 nodes, whose kernels keep
+  two-bit ids.
 * A payload SENT by two different origins is one key in the reference (its dicts are keyed
   by the payload string).  The engine models one sender per key and raises ``EngineError``
   (also when another node first used the payload in an ECHO / READY broadcast).
@@ -111,18 +113,21 @@ def reset():
 
 
 class ValueTable:
-    """Consensus payload strings <-> two-bit value ids; id 0 is str(NONE) == "-1"
-    (core/byzantinerandomizedconsensus.py:68)."""
+    """Consensus payload strings <-> value ids; id 0 is str(NONE) == "-1"
+    (core/byzantinerandomizedconsensus.py:68).  `cap` ids: 8 (three-bit ids) or 4 (include/brc.h
+    brc_injection.value)."""
 
-    def __init__(self):
+    def __init__(self, cap=8):
         self.strings = ["-1"]
+        self.cap = cap
 
     def id_of(self, s):
         s = str(s)
         if s in self.strings:
             return self.strings.index(s)
-        if len(self.strings) == 4:
-            raise L.EngineError(L.E_UNSUPPORTED, "more than 3 distinct proposal values: %r" % (self.strings[1:] + [s]))
+        if len(self.strings) == self.cap:
+            raise L.EngineError(L.E_UNSUPPORTED, "more than %d distinct proposal values: %r"
+                                % (self.cap - 1, self.strings[1:] + [s]))
         self.strings.append(s)
         return len(self.strings) - 1
 
@@ -152,7 +157,10 @@ class Cluster:
         self.key_payload = {}      # (origin, seq) -> payload
         self.seq = {}
         self.sent = set()          # keys SENT (a payload may be declared first by an ECHO / READY)
-        self.values = ValueTable()
+        # three-bit value ids on the narrow kernels that keep them (include/brc.h brc_injection.value)
+        n = len(peers)
+        two_bit = n > 64 or (n > 32 and cfg["peer_mode"] == "sender")
+        self.values = ValueTable(4 if two_bit else 8)
         self.engine = None
         self.seen_events = 0
         self.finished = False
@@ -188,6 +196,10 @@ class Cluster:
             raise ValueError("BEBroadcast and BRBroadcast nodes cannot share a peer list")
         self.beb = True
         self.N, self.f = len(self.peers), 0
+        if self.N > 32:               # best-effort broadcast runs sender peers: two-bit ids past 32 nodes
+            if len(self.values.strings) > 4:
+                raise L.EngineError(L.E_UNSUPPORTED, "more than 3 distinct proposal values on %d nodes" % self.N)
+            self.values.cap = 4
         self.nodes[i] = node
         return i
 

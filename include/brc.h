@@ -113,8 +113,10 @@ typedef struct {
     uint32_t node;            /* proposer / sender */
     uint32_t kp;              /* key slot: origin * variants + variant */
     uint32_t s;               /* phase index 2*(round-1)+(phase-1), or BRB sequence */
-    int32_t value;            /* value id 0..3 (0 == "-1"; larger: BRC_E_INVALID -- two-bit ids, at most
-                                 three distinct proposal values besides "-1") */
+    int32_t value;            /* value id (0 == "-1"): 0..7 on the narrow kernels that keep 3-bit ids
+                                 (n <= 32, or connection peers at n <= 64; not BRC_MODE_SPEC), 0..3 on
+                                 the others (n in 33..64 with sender peers, n > 64, SPEC); larger:
+                                 BRC_E_INVALID.  The same range holds for brc_load_proposals */
     uint64_t dst_mask;        /* BRC_INJ_SEND destinations 0..63; BRC_INJ_MSG must address all
                                  peers (a restricted ECHO / READY: BRC_E_UNSUPPORTED).  A key is
                                  SENT once: a second SEND of it (another origin, as one payload
@@ -177,6 +179,9 @@ int brc_read_round_histogram(void* engine, uint64_t* hist, uint32_t bins);
  * decided; *disagreements counts instances whose honest replicas' first decisions differ
  * (the agreement check of SURVEY §8(e)).  Per engine; shard.reduce_stats all-reduces them. */
 int brc_read_decisions(void* engine, uint64_t* value_hist /* [5] */, uint64_t* disagreements);
+/* The same over 3-bit value ids: value_hist[v] for v = 0..7, value_hist[8] never decided.
+ * brc_read_decisions is BRC_E_STATE once a value id >= 4 was decided. */
+int brc_read_value_decisions(void* engine, uint64_t* value_hist /* [9] */, uint64_t* disagreements);
 /* brc_reset, then re-key the engine to the global instances [instance_offset, +instances): one
  * engine sweeps a range larger than its device footprint in tiles, with the results one engine
  * over the whole range would give (every Philox counter uses the global id).  Loaded proposals

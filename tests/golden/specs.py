@@ -20,6 +20,10 @@ import copy
 import random
 
 VALUES = ["-1", "0", "1", "3"]
+# seven proposal strings besides "-1": the three-bit value ids of the narrow kernels (include/brc.h
+# brc_injection.value); the reference keys its value table by these strings
+# (core/byzantinerandomizedconsensus.py:57-60)
+VALUES8 = ["-1", "0", "1", "3", "alpha", "beta", "gamma", "delta"]
 SEND, ECHO, READY = 1, 2, 3
 
 
@@ -118,12 +122,31 @@ def equivocation_actions(n, byzantine, nv=2, t_send=0, t_er=1):
     return acts
 
 
-def deliver_actions(n, seed, count=None):
+def deliver_actions(n, seed, count=None, nval=4):
     """Direct deliver() calls: replica `node` is handed host `kp`'s message with value id `value`
-    at step t (an action: after step t's messages)."""
+    (0 .. nval-1) at step t (an action: after step t's messages)."""
     rng = random.Random(seed)
     return [dict(t=rng.randint(0, 8), kind="deliver", node=rng.randrange(n), kp=rng.randrange(n),
-                 value=rng.randint(0, 3)) for _ in range(count or 2 * n)]
+                 value=rng.randint(0, nval - 1)) for _ in range(count or 2 * n)]
+
+
+def values8_specs():
+    """More than three distinct proposal strings (VALUES8): majorities of one new string, splits
+    that end in "-1", and direct deliver() calls carrying every id, in both peer modes."""
+    G = {}
+    pats = [[4, 4, 4, 4, 4, 5, 6], [7, 7, 7, 7, 7, 6, 5], [4, 5, 6, 7, 4, 5, 6], [6, 6, 6, 6, 6, 6, 4],
+            [5, 5, 5, 5, 5, 7, 7], [7] * 7]
+    models = ((0, 1), (1, 3), (2, 4), (0, 2), (0, 1), (3, 5))
+    for pm, pre in (("sender", ""), ("connection", "conn_")):
+        G[pre + "cons_values_n7"] = [dict(cons_spec(7, 1, 0x7A10 + g, m, d, g, round_cap=2, proposals=pats[g],
+                                                    peer_mode=pm), values=VALUES8)
+                                     for g, (m, d) in enumerate(models)]
+    rng = random.Random(0x7A16)
+    G["cons_values_deliver_n16"] = [dict(cons_spec(16, 3, 0x7A20 + g, m, d, g, round_cap=2,
+                                                   proposals=[rng.choice((4, 5, 6, 7, 4, 4)) for _ in range(16)],
+                                                   extra=deliver_actions(16, 0x7A30 + g, nval=8)), values=VALUES8)
+                                    for g, (m, d) in enumerate(((0, 1), (0, 2), (1, 4), (2, 3)))]
+    return G
 
 
 def _kat(n, f, seq, byz_nodes, key=(1, 0), name=""):
@@ -306,6 +329,7 @@ def scenario_groups():
                                     for g in range(4)]
     G["conn_cons_uniform_n100"] = [cons_spec(100, 33, 0xC0B1, 1, 4, g, round_cap=1, peer_mode="connection")
                                    for g in range(1)]
+    G.update(values8_specs())
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))

@@ -8,8 +8,9 @@ Supported, checked against the C oracle on the same seeded inputs:
 Rejected with a documented error code (include/brc.h), asserted here:
   * a restricted ECHO / READY injection (BRC_E_UNSUPPORTED): the engine keeps one "sent" time per
     (replica, key, type), so an ECHO that reached only some peers has no representation;
-  * value ids above 3 (BRC_E_INVALID): two-bit value ids, the class API maps at most three
-    distinct proposal strings besides "-1" (network.ValueTable, tested on the CPU);
+  * value ids past the kernel's width (BRC_E_INVALID): three bits on the narrow kernels (n <= 32,
+    connection peers), two on the others; the class API maps at most seven (three) distinct
+    proposal strings besides "-1" (network.ValueTable, tested on the CPU);
   * a second SEND of one key (BRC_E_UNSUPPORTED) -- the ABI form of one payload string SENT by
     two origins (core/brbroadcast.py:76-79 keys its dicts by payload); the class API raises
     EngineError for it before any engine call (tests/test_api_shim.py).
@@ -125,9 +126,11 @@ def test_rejections_are_documented_error_codes(n):
             eng.inject([dict(t=0, kind=L.INJ_SEND, node=1, kp=0, s=0, dst=allm)])
         assert ei.value.code == L.E_UNSUPPORTED
     with _engine(n, protocol="consensus", round_cap=1) as eng:
-        # value ids are two bits: E_INVALID
+        # value ids: three bits on the narrow kernel (n = 16), two on the wide one (n = 100); E_INVALID past them
+        if n <= 32:
+            eng.inject([dict(t=0, kind=L.INJ_PROPOSE, node=0, value=7)])
         with pytest.raises(L.EngineError) as ei:
-            eng.inject([dict(t=0, kind=L.INJ_PROPOSE, node=0, value=4)])
+            eng.inject([dict(t=0, kind=L.INJ_PROPOSE, node=1, value=8 if n <= 32 else 4)])
         assert ei.value.code == L.E_INVALID
 
 

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <string>
 #include <vector>
+#include <unordered_map>
 
 #include "brc_internal.h"
 
@@ -167,6 +168,7 @@ struct Engine {
     unsigned long long* gcount = nullptr;
     uint64_t* dbits = nullptr;                   // lean SPEC: per-wave delivery bitmaps (brc_step.h DBG)
     uint64_t* dring = nullptr;                   // per-link lifetime kernel: delivery bitmap ring (brc_life.h)
+    uint64_t* xsend = nullptr; uint32_t* xsn = nullptr;   // extra-SEND records (non-lean step kernels)
     bool life_pl = false;                        // lifetime kernel in its per-link delay form
     uint32_t nval = 4;                           // consensus value ids the step kernel keeps (value_ids)
     bool values_wide = false;                    // a loaded proposal uses a value id >= 4 (no lifetime kernel)
@@ -178,6 +180,10 @@ struct Engine {
     // per epoch (brc_reset to brc_reset); gen_base sums the epochs since the last full clear
     uint64_t gen_base = 0, gen_cur = 0;
     std::vector<std::pair<uint64_t, uint32_t>> send_keys;   // (instance, kp<<16|s) of injected SENDs
+    struct SendDst { uint64_t inst; uint32_t key, node; uint64_t dst; };
+    std::vector<SendDst> send_dst;               // ... and each sender's destinations (extra SENDs)
+    struct XRec { uint32_t k, t, seg; uint64_t smask, dst; };
+    std::unordered_map<uint64_t, std::vector<XRec>> xrec;   // item -> extra-SEND records (P.xsend)
     // key-lifetime kernel (brc_life.h): eligible configuration, engine fresh since create / reset,
     // and whether the last run used it (its instances are then final: no re-opening injections)
     bool life_cfg = false, fresh = true, life_done = false, last_life = false;
@@ -228,7 +234,7 @@ static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks,
 static void free_all(Engine* e) {
     void* ps[] = {e->cells, e->meta, e->mgen, e->kdst, e->act, e->actany, e->items, e->inst, e->istats,
                   e->cons0, e->cons1, e->hmask, e->inj, e->inj_off, e->inj_cnt, e->byz, e->prop, e->events,
-                  e->event_count, e->gcount, e->dbits, e->dring, e->dparams};
+                  e->event_count, e->gcount, e->dbits, e->dring, e->xsend, e->xsn, e->dparams};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -288,6 +294,7 @@ static int clear_state(Engine* e, bool full) {
     HIPCHK(e, hipMemsetAsync(e->cons1, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * e->cons_bytes, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount, 0, 8 * 8, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->xsn, 0, (size_t)e->nitems * 4, e->stream));
     if (e->event_count) HIPCHK(e, hipMemsetAsync(e->event_count, 0, 8, e->stream));
     return BRC_OK;
 }
@@ -459,6 +466,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
         {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8 : 8},
+        {(void**)&e->xsend, (size_t)e->nitems * XSEND_MAX * 24}, {(void**)&e->xsn, (size_t)e->nitems * 4},
     };
     for (auto& a : allocs)
         if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) {
@@ -540,6 +548,7 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
     std::vector<InjDev> staged;
     std::vector<uint64_t> staged_item;
     std::vector<std::pair<uint64_t, uint32_t>> new_sends;
+    std::vector<Engine::SendDst> new_send_dst;
     for (size_t i = 0; i < count; ++i) {
         const brc_injection& x = list[i];
         if (x.instance >= c.instances || x.node >= c.n || x.t > c.step_cap) { e->err = "injection out of range"; return BRC_E_INVALID; }
@@ -547,6 +556,7 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
             e->err = "value id / phase index out of range (value ids 4..7 need n <= 32 or connection peers, not SPEC)";
             return BRC_E_INVALID;
         }
+        bool drop = false;                       // a repeated SEND carried on no link (sender peers)
         InjDev r = {};
         r.t = x.t; r.kind = (uint8_t)x.kind; r.type = (uint8_t)x.type; r.node = (uint8_t)x.node;
         r.seg = (uint8_t)(x.instance % e->ipw); r.value = (int8_t)x.value; r.s = (uint16_t)x.s;
@@ -571,14 +581,33 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
                 if (x.type != BRC_ECHO && x.type != BRC_READY) { e->err = "MSG type must be ECHO or READY"; return BRC_E_INVALID; }
                 if (!full) { e->err = "ECHO/READY injections must address every peer"; return BRC_E_UNSUPPORTED; }
             } else if (x.kind == BRC_INJ_SEND) {
-                // one SEND per key: a second SEND (other sender / destinations) is not modelled
+                // a second SEND of a key (another origin or the same, one payload string SENT again):
+                // an extra-SEND record on the non-lean step kernels; the lean and wide kernels model
+                // one SEND per key
                 auto key = std::make_pair(x.instance, (uint32_t)(x.kp * 0x10000u + x.s));
-                if (std::find(e->send_keys.begin(), e->send_keys.end(), key) != e->send_keys.end() ||
-                    std::find(new_sends.begin(), new_sends.end(), key) != new_sends.end()) {
-                    e->err = "a key can be SENT only once";
+                if ((e->compact || e->wide) &&
+                    (std::find(e->send_keys.begin(), e->send_keys.end(), key) != e->send_keys.end() ||
+                     std::find(new_sends.begin(), new_sends.end(), key) != new_sends.end())) {
+                    e->err = "a key can be SENT only once on this kernel (n in 33..64 with sender peers, or n > 64)";
                     return BRC_E_UNSUPPORTED;
                 }
                 new_sends.push_back(key);
+                // this node's earlier SENDs of the key (this batch included): r.type = 1 marks a repeat
+                // (brc_step.h: a COPY event with connection peers); sender peers carry a repeated
+                // message on a link no further (the links it used are dropped from the record)
+                uint64_t prev = 0;
+                bool had = false;
+                for (const auto* v : {&e->send_dst, &new_send_dst})
+                    for (const auto& q : *v)
+                        if (q.inst == x.instance && q.key == key.second && q.node == x.node) { prev |= q.dst; had = true; }
+                new_send_dst.push_back({x.instance, key.second, x.node, r.dst});
+                // a key SENT before (by any node): an extra-SEND record (bit 1), bit 0 = this node's repeat
+                const bool again = !(e->compact || e->wide) &&
+                                   (std::find(e->send_keys.begin(), e->send_keys.end(), key) != e->send_keys.end() ||
+                                    std::count(new_sends.begin(), new_sends.end(), key) > 1);
+                r.type = (again ? 2 : 0) | (had ? 1 : 0);
+                if (c.peer_mode == BRC_PEER_SENDER) r.dst &= ~prev;
+                drop = had && r.dst == 0;
             }
         } else {
             e->err = "unknown injection kind";
@@ -599,11 +628,57 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         }
         if (ist[x.instance].status == BRC_QUIESCENT) reopen.push_back(x.instance);
         else if (ist[x.instance].status != BRC_RUNNING) { e->err = "instance already stopped"; return BRC_E_STATE; }
+        if (drop) continue;
         staged.push_back(r);
         staged_item.push_back(item);
     }
+    // extra-SEND records (r.type bit 1) into their items' tables: a record of the same key, step and
+    // destinations without this sender takes it, else one whose arrivals all lie in steps already run,
+    // else a new one; all-or-nothing (a batch that overflows a table changes nothing)
+    std::unordered_map<uint64_t, std::vector<Engine::XRec>> xnew;
+    for (size_t i = 0; i < staged.size(); ++i) {
+        const InjDev& r = staged[i];
+        if (r.kind != BRC_INJ_SEND || !(r.type & 2)) continue;
+        const uint64_t item = staged_item[i];
+        if (!xnew.count(item)) xnew[item] = e->xrec.count(item) ? e->xrec[item] : std::vector<Engine::XRec>();
+        auto& v = xnew[item];
+        int slot = -1, dead = -1;
+        for (size_t j = 0; j < v.size(); ++j) {
+            if (v[j].k == r.slot && v[j].t == r.t && v[j].seg == r.seg && v[j].dst == r.dst && !((v[j].smask >> r.node) & 1ull)) {
+                slot = (int)j;
+                break;
+            }
+            if (dead < 0 && v[j].t + c.delay_max < its[item].t) dead = (int)j;
+        }
+        const Engine::XRec nr = {r.slot, r.t, r.seg, 1ull << r.node, r.dst};
+        if (slot >= 0) v[slot].smask |= 1ull << r.node;
+        else if (dead >= 0) v[dead] = nr;
+        else if (v.size() < XSEND_MAX) v.push_back(nr);
+        else {
+            e->err = "more than " + std::to_string(XSEND_MAX) + " extra-SEND records in flight in one item";
+            return BRC_E_UNSUPPORTED;
+        }
+    }
+    std::vector<uint64_t> xbuf;
+    xbuf.reserve(xnew.size() * (3 * XSEND_MAX + 1));
+    for (auto& kv : xnew) {
+        e->xrec[kv.first] = kv.second;
+        const size_t o = xbuf.size();
+        xbuf.resize(o + 3 * XSEND_MAX + 1, 0);
+        for (size_t j = 0; j < kv.second.size(); ++j) {
+            const auto& q = kv.second[j];
+            xbuf[o + 3 * j] = (uint64_t)q.k | ((uint64_t)q.t << 16) | ((uint64_t)q.seg << 40);
+            xbuf[o + 3 * j + 1] = q.smask;
+            xbuf[o + 3 * j + 2] = q.dst;
+        }
+        xbuf[o + 3 * XSEND_MAX] = kv.second.size();
+        HIPCHK(e, hipMemcpyAsync(e->xsend + kv.first * 3 * XSEND_MAX, &xbuf[o], 3 * XSEND_MAX * 8, hipMemcpyHostToDevice,
+                                 e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->xsn + kv.first, &xbuf[o + 3 * XSEND_MAX], 4, hipMemcpyHostToDevice, e->stream));
+    }
     for (size_t i = 0; i < staged.size(); ++i) e->pending[staged_item[i]].push_back(staged[i]);
     e->send_keys.insert(e->send_keys.end(), new_sends.begin(), new_sends.end());
+    e->send_dst.insert(e->send_dst.end(), new_send_dst.begin(), new_send_dst.end());
     for (uint64_t in : reopen) {
         ist[in].status = BRC_RUNNING;
         HIPCHK(e, hipMemcpyAsync(&e->inst[in], &ist[in], sizeof(InstState), hipMemcpyHostToDevice, e->stream));
@@ -666,7 +741,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount; P.dbits = e->dbits;
-    P.dring = e->dring;
+    P.dring = e->dring; P.xsend = e->xsend; P.xsn = e->xsn;
     const uint32_t blocks = e->wide ? (uint32_t)e->nitems : (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
@@ -705,6 +780,8 @@ int brc_reset(void* h) {
     if (rc) return rc;
     for (auto& v : e->pending) v.clear();
     e->send_keys.clear();
+    e->send_dst.clear();
+    e->xrec.clear();
     if (e->pattern_active) {
         e->pattern_active = false;
         rc = apply_pattern(e);

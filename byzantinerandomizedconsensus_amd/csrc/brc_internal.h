@@ -20,6 +20,7 @@ constexpr uint32_t F_EEX = 1, F_REX = 2, F_DEL = 4, F_ES = 8, F_RS = 16;
 constexpr uint32_t GEN_MASK = 0x1FFF;
 constexpr uint32_t GEN_RESTRICTED = 0x80000000u;
 constexpr uint32_t GEN16_RESTRICTED = 0x8000u;  // the narrow kernel's 16-bit LDS copy of mgen
+constexpr uint32_t GEN16_XDONE = 0x4000u;       // ... key processed by this step's extra-SEND pre-pass (brc_step.h)
 __host__ __device__ inline uint16_t gen16(uint32_t g) {
     return (uint16_t)((g & GEN_MASK) | ((g & GEN_RESTRICTED) ? GEN16_RESTRICTED : 0u));
 }
@@ -100,6 +101,8 @@ struct Params {
     brc_event* events; unsigned long long* event_count;
     uint64_t* dbits;              // lean SPEC: per-wave delivery bitmaps [item][nkw][64] (brc_step.h DBG)
     uint64_t* dring;              // per-link key-lifetime kernel: delivery bitmap ring [item][LIFE_RW][nkw][64] (brc_life.h)
+    uint64_t* xsend;              // non-lean step kernels: extra-SEND records [item][XSEND_MAX][3] (brc_step.h)
+    uint32_t* xsn;                // ... records in use per item
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
                                   // [6] instances still running after the launch
 };
@@ -108,6 +111,9 @@ struct Params {
 __host__ __device__ inline uint32_t delay_values(uint32_t model, uint32_t dmax) {
     return model == BRC_DELAY_CONST ? 1u : model == BRC_DELAY_SLOWSET ? (dmax > 1 ? 2u : 1u) : dmax;
 }
+
+// Extra-SEND records per item (a payload SENT by several origins; brc_step.h): live at once
+constexpr uint32_t XSEND_MAX = 16;
 
 // Consensus value ids (core/byzantinerandomizedconsensus.py:57-60 keys its tables by payload string;
 // id 0 is str(NONE) == "-1"): 2 bits (3 strings + "-1") on the lean, wide and key-lifetime kernels,

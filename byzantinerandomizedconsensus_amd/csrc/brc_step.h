@@ -683,6 +683,15 @@ void brc_step(const Params* __restrict__ pp) {
     uint32_t dcount = c1 & 0xFFFF, frnd = (c1 >> 16) & 0xFFFF, ft = (c1 >> 32) & 0xFFFF;
     uint32_t fval = (c1 >> 48) & 0xFF, lval = (c1 >> 56) & 0xFF;
 
+    // Extra SENDs of a key already SENT (one payload string SENT by several origins, or again: the
+    // reference keys its BRB state by payload, core/brbroadcast.py:38-44, :76-82), non-lean kernels:
+    // per item XSEND_MAX records {k | t << 16 | seg << 40, sender mask, dst mask} in HBM (P.xsend,
+    // written by brc_inject), xs_n in use (P.xsn).  Sender j of a record lands on receiver d at
+    // t + delay(j -> d), as the key's own SEND; SENDs of one key at one step to one destination set
+    // share a record.  (Sender peers: brc_inject has removed the links a sender used before.)
+    uint32_t xs_n = LEAN ? 0u : uni32(gp(P.xsn)[item]);
+    auto xs_ld = [&](uint32_t i) -> uint64_t { return uni64(gp(P.xsend)[item * (uint64_t)(3 * XSEND_MAX) + i]); };
+
     uint32_t st_msgs = 0, st_arr = 0, st_cells = 0, st_del = 0, st_loads = 0, st_smax = 0;
     uint32_t st_bcast = 0;                       // lean path: ECHO/READY broadcasts (n messages each)
     // lean path, wave-uniform: key list entries (nk_lean) minus empty slots among them (nk_skip)
@@ -971,7 +980,26 @@ void brc_step(const Params* __restrict__ pp) {
                         if ((Lmask(j) >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
                 }
                 const uint32_t os = wave_or(myset);
-                if (mine) {
+                // a SEND of a key already SENT (another origin or again, one payload): brc_inject has
+                // put it in the item's extra-SEND records (r.type bit 1; bit 0: a repeat of this node's)
+                if (!LEAN && (r.type & 2u)) {
+                    if (mine && d == 0) {
+                        const uint32_t k = r.slot;
+                        const uint64_t m = s_meta[mbase + k];
+                        if (m_s1(m) != r.s + 1u || m_tsend(m) == NEVER) {
+                            badinj = true;                   // the key is not the SENT one brc_inject saw
+                        } else {
+                            if (t + hibit(os) > m_tquiet(m)) s_meta[mbase + k] = m_with_tquiet(m, t + hibit(os));
+                            mark_lane(k, os, BRC_SEND);
+                            st_msgs += __popcll(r.dst & all64);
+                            // a node's first SEND of the key is a SEND event; a repeat is a COPY event with
+                            // connection peers and none with sender peers (as for any duplicate)
+                            if (!(r.type & 1u)) log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, m_value(m));
+                            else if (CONN) log_ev(BRC_EV_COPY, r.node, BRC_SEND, (k >> qsh), r.s, m_value(m));
+                        }
+                    }
+                    if (mine) q_until = max(q_until, t + hibit(os));
+                } else if (mine) {
                     const uint32_t k = r.slot;
                     bool fresh = false;                  // lean: the slot is (re)allocated: fresh row
                     if (d == 0) {
@@ -1481,7 +1509,8 @@ void brc_step(const Params* __restrict__ pp) {
                 }
             }
         };
-        auto process = [&](const uint32_t k, const uint64_t wd) {
+        // xsa: this lane's extra-SEND arrivals of key k (the pre-pass below; 0 in the key loop)
+        auto process = [&](const uint32_t k, const uint64_t wd, const uint32_t xsa) {
             // both LDS reads issue before either is waited on (k == NK, the trash row: junk, unused)
             const uint64_t m_raw = s_meta[mbase + k];
             const uint32_t gw_raw = s_gen[mbase + k];
@@ -1489,7 +1518,8 @@ void brc_step(const Params* __restrict__ pp) {
             uint32_t gw = gw_raw;
             if (IPW == 1) { m = uni64(m); gw = uni32(gw); }      // one instance per wave
             const uint32_t gen = gw & GEN_MASK;
-            const bool kl = k < NK && m_s1(m) != 0;              // the slot holds a key
+            // the slot holds a key (not one the extra-SEND pre-pass processed this step)
+            const bool kl = k < NK && m_s1(m) != 0 && (LEAN || !(gw & GEN16_XDONE));
             const bool live = kl && running;
             const bool cur = kl && real_run && (((uint32_t)wd >> 19) & GEN_MASK) == gen;
             const uint64_t word = cur ? wd : TIMES_NEVER;
@@ -1539,6 +1569,8 @@ void brc_step(const Params* __restrict__ pp) {
                     hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = s_win && hon_run && hit;
             }
+            const uint32_t sa = (LEAN ? 0u : xsa) + (s_arr ? 1u : 0u);   // SEND arrivals (extra SENDs: several)
+            s_arr = sa != 0;
             const bool has = kl && hon_run && (s_arr || ea || ra);
             st_loads += (kl && real_run) ? 1u : 0u;
             uint32_t fl = (uint32_t)word & 31, ec = (uint32_t)(word >> 5) & 127, rc = (uint32_t)(word >> 12) & 127;
@@ -1575,7 +1607,7 @@ void brc_step(const Params* __restrict__ pp) {
                 mycells[(size_t)k * (CW * 64)] = has ? nw : wd;  // whole-wave store (unchanged words back)
 #endif
             }
-            st_arr += has ? ea + ra + (s_arr ? 1u : 0u) : 0u;
+            st_arr += has ? ea + ra + sa : 0u;
             st_cells += has ? 1u : 0u;
             st_msgs += ((es ? 1u : 0u) + (CONN ? n_ready : (rs ? 1u : 0u))) * n;
             st_del += dl ? 1u : 0u;
@@ -1685,6 +1717,40 @@ void brc_step(const Params* __restrict__ pp) {
                 });
             }
         } else {
+            // Extra-SEND pre-pass (records of keys SENT again, rare): a key with extra SEND arrivals
+            // now is processed here, whole (its SENDs ahead of its ECHO / READY, the canonical
+            // order), with the arrival count summed over its records; the key loop then skips it
+            // (GEN16_XDONE, cleared after the loop).  No code of this is in the key loop's process().
+            auto xs_active = [&](uint64_t w0) -> bool {
+                const uint32_t dt2 = t - ((uint32_t)(w0 >> 16) & 0xFFFFu);
+                return dt2 - 1u < D && ((dset >> ((dt2 - 1u) & 31)) & 1u);
+            };
+            if (xs_n) {
+                for (uint32_t i = 0; i < xs_n; ++i) {
+                    const uint64_t w0 = xs_ld(3 * i);
+                    const uint32_t k = (uint32_t)(w0 & 0xFFFFu);
+                    if (!xs_active(w0)) continue;
+                    bool seen = false;                   // an earlier active record of this slot
+                    for (uint32_t j = 0; j < i; ++j) {
+                        const uint64_t v0 = xs_ld(3 * j);
+                        seen = seen || ((uint32_t)(v0 & 0xFFFFu) == k && xs_active(v0));
+                    }
+                    if (seen) continue;
+                    uint32_t xsa = 0;
+                    for (uint32_t j = i; j < xs_n; ++j) {
+                        const uint64_t v0 = xs_ld(3 * j);
+                        if ((uint32_t)(v0 & 0xFFFFu) != k || !xs_active(v0)) continue;
+                        const uint32_t dt2 = t - ((uint32_t)(v0 >> 16) & 0xFFFFu), b2 = 1u << (dt2 - 1u);
+                        const uint64_t snd = xs_ld(3 * j + 1), dst2 = xs_ld(3 * j + 2);
+                        const bool mine2 = hon_run && seg == (int)((v0 >> 40) & 0xFF) && ((dst2 >> d) & 1ull);
+                        xsa += mine2 ? popc((T)(Lmask(popc(dset & (b2 - 1u))) & (T)snd)) : 0u;
+                    }
+                    process(k, mycells[(size_t)k * (CW * 64)], xsa);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    if (d == 0) s_gen[mbase + k] |= GEN16_XDONE;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                }
+            }
             uint64_t wA[CHUNK];
             uint32_t kA[CHUNK];
             fetch(0, wA, kA);
@@ -1694,13 +1760,21 @@ void brc_step(const Params* __restrict__ pp) {
                 fetch(p + CHUNK, wB, kB);
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
-                    process(kA[c], wA[c]);                       // padding slots: the trash row
+                    process(kA[c], wA[c], 0u);                   // padding slots: the trash row
                 });
                 Unrolled<CHUNK>::run([&](auto ci) {
                     constexpr int c = decltype(ci)::value;
                     wA[c] = wB[c];
                     kA[c] = kB[c];
                 });
+            }
+            if (xs_n) {
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                for (uint32_t i = 0; i < xs_n; ++i) {
+                    const uint64_t w0 = xs_ld(3 * i);
+                    if (xs_active(w0) && d == 0) s_gen[mbase + (uint32_t)(w0 & 0xFFFFu)] &= (uint16_t)~GEN16_XDONE;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
         }
         BRC_STAMP(1);

@@ -24,9 +24,11 @@ Deviations from the reference, all reported by exceptions and never silent:
 * At most seven distinct proposal strings besides ``"-1"`` (three-bit value ids) -- three on
   clusters of 33..64 nodes with ``peer_mode="sender"`` and above 64 nodes, whose kernels keep
   two-bit ids.
-* A payload SENT by two different origins is one key in the reference (its dicts are keyed
-  by the payload string).  The engine models one sender per key and raises ``EngineError``
-  (also when another node first used the payload in an ECHO / READY broadcast).
+* A payload SENT by two different origins (or SENT again) is one key in the reference (its
+  dicts are keyed by the payload string); the engine models it as one key with extra SENDs
+  (brc_step.h extra-SEND records, up to 8 in flight) on clusters up to 32 nodes and with
+  connection peers up to 64; on the others (33..64 nodes with sender peers, more than 64) it
+  raises ``EngineError``.
 * ``broadcast(type, m)`` takes SEND, ECHO and READY (the reference also puts other types on
   the wire, which its handler then ignores): other types raise ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
@@ -159,8 +161,9 @@ class Cluster:
         self.sent = set()          # keys SENT (a payload may be declared first by an ECHO / READY)
         # three-bit value ids on the narrow kernels that keep them (include/brc.h brc_injection.value)
         n = len(peers)
-        two_bit = n > 64 or (n > 32 and cfg["peer_mode"] == "sender")
-        self.values = ValueTable(4 if two_bit else 8)
+        # the lean (33..64 nodes, sender peers) and wide (> 64) kernels: two-bit value ids, one SEND per key
+        self.lean_or_wide = n > 64 or (n > 32 and cfg["peer_mode"] == "sender")
+        self.values = ValueTable(4 if self.lean_or_wide else 8)
         self.engine = None
         self.seen_events = 0
         self.finished = False
@@ -200,6 +203,7 @@ class Cluster:
             if len(self.values.strings) > 4:
                 raise L.EngineError(L.E_UNSUPPORTED, "more than 3 distinct proposal values on %d nodes" % self.N)
             self.values.cap = 4
+            self.lean_or_wide = True
         self.nodes[i] = node
         return i
 
@@ -232,12 +236,11 @@ class Cluster:
             raise L.EngineError(L.E_UNSUPPORTED, "raw BRB SENDs on a consensus cluster")
         payload = str(payload)
         key = self._key_of(i, payload)
-        if key[0] != i:
-            raise L.EngineError(L.E_UNSUPPORTED, "payload %r SENT by two origins (one reference key)" % payload)
-        if key in self.sent:
-            return                # identical message on the same links: suppressed
+        if (key[0] != i or key in self.sent) and self.lean_or_wide:
+            raise L.EngineError(L.E_UNSUPPORTED, "payload %r SENT twice (one reference key) on a %d-node cluster "
+                                "with %s peers" % (payload, len(self.peers), self.cfg["peer_mode"]))
         self.sent.add(key)
-        self.actions.append(dict(t=self.t, kind=L.INJ_SEND, node=i, kp=i, s=key[1], value=0,
+        self.actions.append(dict(t=self.t, kind=L.INJ_SEND, node=i, kp=key[0], s=key[1], value=0,
                                  dst=(1 << len(self.peers)) - 1))
 
     def brb_msg(self, i, message_type, payload):

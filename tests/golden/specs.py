@@ -330,9 +330,33 @@ def scenario_groups():
     G["conn_cons_uniform_n100"] = [cons_spec(100, 33, 0xC0B1, 1, 4, g, round_cap=1, peer_mode="connection")
                                    for g in range(1)]
     G.update(values8_specs())
+    G.update(multisend_specs())
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))
+    return G
+
+
+def multisend_specs():
+    """One payload string SENT by several nodes, and SENT again by its own node (the reference keys
+    BRB state by payload, core/brbroadcast.py:38-44, :76-82): one key, extra SENDs, both peer modes."""
+    G = {}
+    extra = [dict(t=0, kind="brb_send", node=3, kp=0, s=0, payload="TEST 1.0"),
+             dict(t=1, kind="brb_send", node=4, kp=0, s=0, payload="TEST 1.0"),
+             dict(t=3, kind="brb_send", node=1, kp=1, s=0, payload="TEST 2.0"),
+             dict(t=2, kind="brb_send", node=5, kp=2, s=0, payload="TEST 3.0"),
+             dict(t=2, kind="brb_send", node=6, kp=2, s=0, payload="TEST 3.0")]
+    models = ((0, 1), (1, 3), (2, 4), (3, 5))
+    for pm, pre in (("sender", ""), ("connection", "conn_")):
+        G[pre + "brb_multisend_n7"] = [
+            brb_spec(7, 2, 0x3A10 + g, m, d, g, [(0, 0, 0), (0, 1, 0), (2, 2, 0)], extra=extra, peer_mode=pm)
+            for g, (m, d) in enumerate(models)]
+    # payloads SENT by every node at once, and one SENT only by others after its origin crashed
+    crash = [dict(t=0, kind="brb_send", node=o, kp=0, s=0, payload="TEST 1.0") for o in range(1, 16)]
+    G["brb_multisend_n16"] = [brb_spec(16, 5, 0x3A20 + g, m, d, g, [(0, 0, 0), (1, 7, 0)], byzantine=[15],
+                                       extra=crash[:14] + [dict(t=2, kind="brb_send", node=3, kp=7, s=0,
+                                                                payload="TEST 8.0")])
+                              for g, (m, d) in enumerate(((1, 4), (2, 8), (3, 6)))]
     return G
 
 

@@ -82,14 +82,16 @@ def test_brb_sends_become_injections():
     for nd in nodes:
         nd.broadcast_listener()
     nodes[2].broadcast(BRBroadcast.SEND, "A")
-    nodes[2].broadcast(BRBroadcast.SEND, "A")      # identical message: suppressed by the network
+    nodes[2].broadcast(BRBroadcast.SEND, "A")      # the same message again: every link carries it again
     nodes[2].broadcast(BRBroadcast.SEND, "B")
     c = nodes[0].cluster
     assert all(nd.cluster is c for nd in nodes)
-    assert [(a["node"], a["kp"], a["s"], a["t"]) for a in c.actions] == [(2, 2, 0, 0), (2, 2, 1, 0)]
+    assert [(a["node"], a["kp"], a["s"], a["t"]) for a in c.actions] == [(2, 2, 0, 0), (2, 2, 0, 0), (2, 2, 1, 0)]
     assert c.key_payload == {(2, 0): "A", (2, 1): "B"}
-    with pytest.raises(L.EngineError):
-        nodes[1].broadcast(BRBroadcast.SEND, "A")  # one reference key, two origins
+    nodes[1].broadcast(BRBroadcast.SEND, "A")      # one reference key, a second origin: an extra SEND
+    assert (c.actions[-1]["node"], c.actions[-1]["kp"], c.actions[-1]["s"]) == (1, 2, 0)
+    del c.actions[-1]
+    del c.actions[1]
     # user-issued ECHO / READY (base/broadcast.py:17): the payload's key, every peer addressed;
     # a payload nobody SENT is declared first under the caller's next sequence number
     nodes[1].broadcast(BRBroadcast.ECHO, "A")
@@ -99,8 +101,8 @@ def test_brb_sends_become_injections():
     assert acts == [(L.INJ_MSG, BRBroadcast.ECHO, 1, 2, 0), (L.INJ_KEY, 0, 3, 3, 0),
                     (L.INJ_MSG, BRBroadcast.READY, 3, 3, 0), (L.INJ_SEND, 0, 3, 3, 0)]
     assert all(a["dst"] == 15 for a in c.actions if a["kind"] != L.INJ_KEY)
-    with pytest.raises(L.EngineError):
-        nodes[0].broadcast(BRBroadcast.SEND, "C")  # declared by node 3
+    nodes[0].broadcast(BRBroadcast.SEND, "C")      # declared by node 3, SENT by 3 and now by 0
+    assert (c.actions[-1]["kind"], c.actions[-1]["node"], c.actions[-1]["kp"]) == (L.INJ_SEND, 0, 3)
     with pytest.raises(L.EngineError):
         nodes[0].broadcast(7, "D")                 # the engine carries SEND / ECHO / READY only
     with pytest.raises(ValueError):

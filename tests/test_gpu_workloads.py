@@ -11,9 +11,11 @@ Rejected with a documented error code (include/brc.h), asserted here:
   * value ids past the kernel's width (BRC_E_INVALID): three bits on the narrow kernels (n <= 32,
     connection peers), two on the others; the class API maps at most seven (three) distinct
     proposal strings besides "-1" (network.ValueTable, tested on the CPU);
-  * a second SEND of one key (BRC_E_UNSUPPORTED) -- the ABI form of one payload string SENT by
-    two origins (core/brbroadcast.py:76-79 keys its dicts by payload); the class API raises
-    EngineError for it before any engine call (tests/test_api_shim.py).
+  * a second SEND of one key on the lean (n in 33..64, sender peers) and wide (n > 64) kernels
+    (BRC_E_UNSUPPORTED) -- the ABI form of one payload string SENT by two origins
+    (core/brbroadcast.py:76-79 keys its dicts by payload); the other narrow kernels take it as an
+    extra SEND (reference fixtures brb_multisend_*); the class API raises EngineError for it
+    before any engine call on the former (tests/test_api_shim.py).
 """
 import random
 
@@ -111,7 +113,7 @@ def _engine(n, **kw):
     return Engine(**args)
 
 
-@pytest.mark.parametrize("n", [16, 100])
+@pytest.mark.parametrize("n", [16, 40, 100])
 def test_rejections_are_documented_error_codes(n):
     from byzantinerandomizedconsensus_amd import _lib as L
     allm = (1 << n) - 1
@@ -121,10 +123,14 @@ def test_rejections_are_documented_error_codes(n):
         with pytest.raises(L.EngineError) as ei:
             eng.inject([dict(t=1, kind=L.INJ_MSG, type=L.ECHO, node=1, kp=0, s=0, dst=allm & ~2)])
         assert ei.value.code == L.E_UNSUPPORTED
-        # a second SEND of the same key (one payload, two origins): E_UNSUPPORTED
-        with pytest.raises(L.EngineError) as ei:
+        # a second SEND of the same key (one payload, two origins): an extra SEND at n <= 32,
+        # E_UNSUPPORTED on the lean (n = 40) and wide (n = 100) kernels
+        if n <= 32:
             eng.inject([dict(t=0, kind=L.INJ_SEND, node=1, kp=0, s=0, dst=allm)])
-        assert ei.value.code == L.E_UNSUPPORTED
+        else:
+            with pytest.raises(L.EngineError) as ei:
+                eng.inject([dict(t=0, kind=L.INJ_SEND, node=1, kp=0, s=0, dst=allm)])
+            assert ei.value.code == L.E_UNSUPPORTED
     with _engine(n, protocol="consensus", round_cap=1) as eng:
         # value ids: three bits on the narrow kernel (n = 16), two on the wide one (n = 100); E_INVALID past them
         if n <= 32:

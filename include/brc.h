@@ -118,9 +118,12 @@ typedef struct {
                                  the others (n in 33..64 with sender peers, n > 64, SPEC); larger:
                                  BRC_E_INVALID.  The same range holds for brc_load_proposals */
     uint64_t dst_mask;        /* BRC_INJ_SEND destinations 0..63; BRC_INJ_MSG must address all
-                                 peers (a restricted ECHO / READY: BRC_E_UNSUPPORTED).  A key is
-                                 SENT once: a second SEND of it (another origin, as one payload
-                                 string SENT by two nodes would be) is BRC_E_UNSUPPORTED */
+                                 peers (a restricted ECHO / READY: BRC_E_UNSUPPORTED).  A second
+                                 SEND of a key (another node, or the same again: one payload string
+                                 SENT twice, one key in the reference) is an extra SEND on the
+                                 narrow kernels that keep 3-bit value ids (up to 16 extra-SEND
+                                 records in flight per wave item; it must not precede the key's
+                                 first SEND); BRC_E_UNSUPPORTED on the others */
     uint64_t dst_mask_hi[3];  /* destinations 64..255 (n > 64), as byzantine_mask_hi */
 } brc_injection;
 

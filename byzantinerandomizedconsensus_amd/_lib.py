@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
 LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 OK, E_INVALID, E_NOMEM, E_HIP, E_UNSUPPORTED, E_STATE = 0, -1, -2, -3, -4, -5
 ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP error",

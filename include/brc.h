@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 5
+#define BRC_ABI_VERSION 6
 
 enum {
     BRC_OK = 0,

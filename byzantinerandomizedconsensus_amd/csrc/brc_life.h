@@ -92,11 +92,18 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
     const uint64_t real_mask = (n >= 64) ? ~0ull : ((1ull << n) - 1);
     const uint64_t hon_mask = uni64(__ballot(honest));
     auto lane_in = [](uint64_t mask) -> bool { return __builtin_amdgcn_inverse_ballot_w64(mask); };
+    // wave sum through DPP row butterflies and four lane reads (VALU; the kernel is SALU-bound).
+    // Every lane active (the kernel's wave-level code never diverges around it).
     auto wave_sum = [](uint32_t x) -> uint32_t {
-#pragma unroll
-        for (int o = 32; o; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
-        return uni32(x);
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);    // quad_perm [1,0,3,2]
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);    // quad_perm [2,3,0,1]
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);   // row_half_mirror
+        x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);   // row_mirror
+        return uni32(rl(x, 0) + rl(x, 16) + rl(x, 32) + rl(x, 48));
     };
+    // per-row statistics of the step ring in lane registers (lane = row < RW): arrivals, messages,
+    // cells, deliveries -- a select per key-step instead of an exec-masked LDS read-modify-write
+    uint32_t rg_arr = 0, rg_msg = 0, rg_cell = 0, rg_del = 0;
 
     // ---- two delay classes: delay(j -> d) = 1 if j and d are both fast, Dd otherwise
     uint64_t Fm = 0;                               // real fast replicas (PL: none, Dd unused)
@@ -147,7 +154,6 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) { s_meta[i] = 0; s_snap[i] = 0; }
     for (uint32_t i = lane; i < 2 * RW * nkw; i += 64) s_dkA[i] = 0;
-    for (uint32_t i = lane; i < 2 * RW; i += 64) s_ring[i] = 0;
     if constexpr (SPEC) {
         for (uint32_t q = 0; q < Q; ++q) {
             if (seen_on) s_seen[q * 64 + lane] = 0;
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
         uint32_t fl = 0, ec = 0, rc = 0, rE = LIFE_NEVER, rR = LIFE_NEVER;
         Ring16 ringR = {0ull, 0ull};                  // PL connection peers: READY copies per step
         uint32_t last = t0;
-        if constexpr (CONN) s_pr[lane] = 0;
+        uint32_t prv = 0;                             // CONN two-class: READY copies landing at relative step = lane
         const uint32_t kw = k >> 6;
         const uint64_t kbit = 1ull << (k & 63);
         for (uint64_t pend = pendS; pend; pend = pendS | pendE | pendR) {
@@ -338,7 +344,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
             }
             if (hR) {
                 if constexpr (CONN) {
-                    const uint32_t ab = uni32(s_pr[r]);
+                    const uint32_t ab = uni32(rl(prv, (int)r));
                     rA = ab & 0xFFFFu; rB = ab >> 16;
                 } else {
                     const uint64_t x1 = __ballot(rR == c1), xD = __ballot(rR == cD);
@@ -420,13 +426,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
             // READY messages sent now by fast / slow senders (CONN: copies, a lane may send several)
             uint32_t cF = (uint32_t)__popcll(rbm & Fm), cS = (uint32_t)__popcll(rbm & Sm);
             if constexpr (CONN) {
-                if (__ballot(nr > 1)) {                                  // bit planes of the per-lane counts
-                    cF = cS = 0;
-                    for (uint32_t b = 0; b < 8; ++b) {
-                        const uint64_t pb = __ballot((nr >> b) & 1u);
-                        cF += (uint32_t)__popcll(pb & Fm) << b;
-                        cS += (uint32_t)__popcll(pb & Sm) << b;
-                    }
+                if (__ballot(nr > 1)) {                                  // per-class sums of the per-lane counts
+                    const uint32_t pk = wave_sum(laneF ? nr : nr << 16);   // <= 64 x 255 per half
+                    cF = pk & 0xFFFFu; cS = pk >> 16;
                 }
             }
             const uint32_t msgs = n * ((uint32_t)__popcll(eb) + cF + cS);
@@ -460,15 +462,14 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
                 if (at1) pendR |= rb << 1;
                 if (atD) pendR |= rb << Dd;
                 if constexpr (CONN) {
-                    if (lane == 0) {
-                        if (at1) s_pr[r + 1] += cF;
-                        if (atD) s_pr[r + Dd] += cS + ((cF + cS) << 16);
-                    }
+                    if (at1) prv += lane == r + 1 ? cF : 0u;
+                    if (atD) prv += lane == r + Dd ? cS + ((cF + cS) << 16) : 0u;
                 }
             }
-            if (lane == 0) {
-                s_ring[2 * row] += (uint64_t)arr | ((uint64_t)msgs << 32);
-                s_ring[2 * row + 1] += (uint64_t)cells | ((uint64_t)dels << 32);
+            {
+                const bool mine = lane == row;
+                rg_arr += mine ? arr : 0u; rg_msg += mine ? msgs : 0u;
+                rg_cell += mine ? cells : 0u; rg_del += mine ? dels : 0u;
             }
             rows |= 1u << row;
             last = ts;
@@ -515,9 +516,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
         const uint32_t row = t & (RW - 1);
         // commit the step's statistics
         {
-            const uint64_t a = s_ring[2 * row], c = s_ring[2 * row + 1];
-            tot_arr += (uint32_t)a; tot_msg += a >> 32; tot_cell += (uint32_t)c; tot_del += c >> 32;
-            if ((uint32_t)c) t_stop = t;
+            const uint32_t a = uni32(rl(rg_arr, (int)row)), mg = uni32(rl(rg_msg, (int)row));
+            const uint32_t ce = uni32(rl(rg_cell, (int)row)), de = uni32(rl(rg_del, (int)row));
+            tot_arr += a; tot_msg += mg; tot_cell += ce; tot_del += de;
+            if (ce) t_stop = t;
         }
         // ================= consensus: this step's deliveries in canonical (kp, s) order
         for (uint32_t i = lane; i < NK; i += 64) s_snap[i] = (uint16_t)s_meta[i];
@@ -617,7 +619,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
         msg_now = 0;
         // the step is consumed: its ring row is free for step t + RW
         if (lane < 2 * nkw) (lane < nkw ? s_dkA : s_dkB)[row * nkw + (lane % nkw)] = 0;
-        if (lane < 2) s_ring[2 * row + lane] = 0;
+        if (lane == row) { rg_arr = 0; rg_msg = 0; rg_cell = 0; rg_del = 0; }
         rows &= ~(1u << row);
         // ================= per-instance stop conditions (brc_step.h)
         const uint64_t b_und = __ballot(honest && dcount < P.round_cap);

@@ -367,12 +367,31 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
             uint32_t es = 0, rs = 0, dl = 0, nr = 0;
             if constexpr (CONN) {
                 // core/brbroadcast.py:60-119 with connection-identity peers (brc_step.h brb_cell_update_conn):
-                // sets count messages; the :119 amplification re-fires, nr READY copies this step
-                bool esb, dlb;
-                brb_cell_update_conn(fl, ec, rc, opn && sa, opn ? ea : 0u, opn ? ra : 0u, T_echo, T_amp, T_del, esb, nr,
-                                     dlb);
-                fl |= nr ? F_RS : 0u;
-                es = esb ? 1u : 0u; rs = nr ? 1u : 0u; dl = dlb ? 1u : 0u;
+                // sets count messages; the :119 amplification re-fires, nr READY copies this step.  In
+                // integer form (0/1 words, VALU): the bool form's per-lane conditions became SGPR lane
+                // masks combined with scalar ANDs, and this kernel is SALU-bound.
+                const uint32_t o = opn ? 1u : 0u, om = 0u - o;
+                es = o & sa & ~fl & 1u;                                   // :76-82 (F_EEX = bit 0)
+                fl |= es | (es << 3);
+                const uint32_t e = ea & om, eon = min(e, 1u);             // :84-98
+                const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
+                fl |= eon;
+                ec += e;
+                const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
+                fl |= r1 << 1;
+                const uint32_t x = ra & om, ron = min(x, 1u);             // :100-119
+                const uint32_t rexm = 0u - ((fl >> 1) & 1u);
+                const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
+                fl |= ron << 1;
+                rc += x;
+                const uint32_t any = ron & ge(rhi, rlo);
+                const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+                const uint32_t fire = any & ~fl & ge(ahi, alo) & 1u;      // :118 (no F_RS test: re-fires)
+                nr = r1 + ((ahi - alo + 1u) & (0u - fire));
+                dl = any & ge(rhi, T_del);                                // :111-115
+                fl |= dl << 2;
+                rs = min(nr, 1u);
+                fl |= rs << 4;
             } else if constexpr (BEB) {
                 dl = (opn && sa) ? 1u : 0u;                             // brb_cell_update_beb
                 fl |= dl << 2;

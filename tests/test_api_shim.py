@@ -350,3 +350,25 @@ def test_more_than_three_proposal_strings_match_reference(group):
         status = cluster.run()
         assert status == case["result"]["status"], sp["name"]
         assert got == [[t, node, v] for (t, node, _r, v) in sorted(case["result"]["events"]["decide"])], sp["name"]
+
+
+def test_repeated_send_refused_where_the_kernel_keeps_one_send_per_key():
+    """Clusters of 33..64 nodes with sender peers (lean kernel) and above 64 nodes (wide kernel)
+    model one SEND per key: a payload SENT again, or by a second node, raises before any engine call."""
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    for n, pm, ok in ((40, "sender", False), (40, "connection", True), (70, "connection", False), (16, "sender", True)):
+        network.reset()
+        network.configure(peer_mode=pm)
+        try:
+            peers = _peers(n, 7000)
+            nodes = [BRBroadcast(n, (n - 1) // 3, p, peers, None) for p in peers[:3]]
+            nodes[0].broadcast(BRBroadcast.SEND, "P")
+            if ok:
+                nodes[1].broadcast(BRBroadcast.SEND, "P")
+                assert len(nodes[0].cluster.actions) == 2
+            else:
+                with pytest.raises(L.EngineError):
+                    nodes[1].broadcast(BRBroadcast.SEND, "P")
+        finally:
+            network.reset()
+            network.configure(peer_mode="connection")

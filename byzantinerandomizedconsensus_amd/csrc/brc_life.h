@@ -167,7 +167,14 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
     uint32_t status = BRC_RUNNING, t_stop = 0, t = 0;
     bool ovf = false;
     // committed statistics (wave-uniform) and per-lane work counters
-    uint64_t tot_arr = 0, tot_msg = 0, tot_cell = 0, tot_del = 0, key_steps = 0;
+    // per-instance totals in one lane-distributed register (lane 0 messages, 1 arrivals, 2 cells,
+    // 3 deliveries, 4 key-steps): VALU selects instead of five uniform 64-bit SGPR pairs live
+    // through the kernel (it is SALU- and SGPR-bound)
+    uint64_t acc = 0;
+    auto acc_add = [&](uint32_t l, uint32_t v) { acc += (lane == l) ? (uint64_t)v : 0ull; };
+    auto acc_get = [&](int l) -> uint64_t {
+        return ((uint64_t)uni32(rl((uint32_t)(acc >> 32), l)) << 32) | uni32(rl((uint32_t)acc, l));
+    };
     uint32_t st_smax = 0;
     uint32_t rows = 0;                             // ring rows holding arrivals at honest receivers
 
@@ -300,7 +307,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
             pendS &= ~rb; pendE &= ~rb; pendR &= ~rb;
             if (r > RW) { ovf = true; break; }        // two-class: cannot happen for Dd <= 8 (lifetime <= 4 Dd)
             const uint32_t ts = t0 + r, row = ts & (RW - 1);
-            ++key_steps;
+            acc_add(4u, 1u);
             // arrival counts per receiver class (fast: fast senders at r - 1, slow senders at r - Dd;
             // slow: every sender at r - Dd), then per lane
             const uint32_t c1 = r - 1u, cD = r >= Dd ? r - Dd : 0xFFFFFFFFu;
@@ -518,7 +525,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
         if constexpr (SPEC) spec_advance();
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    tot_msg += wave_sum(msg_now);
+    acc_add(0u, wave_sum(msg_now));
     msg_now = 0;
     if (__ballot(ovf)) status = BRC_OVERFLOW;
     else simulate_new();
@@ -537,7 +544,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
         {
             const uint32_t a = uni32(rl(rg_arr, (int)row)), mg = uni32(rl(rg_msg, (int)row));
             const uint32_t ce = uni32(rl(rg_cell, (int)row)), de = uni32(rl(rg_del, (int)row));
-            tot_arr += a; tot_msg += mg; tot_cell += ce; tot_del += de;
+            acc += lane == 0 ? (uint64_t)mg : lane == 1 ? (uint64_t)a : lane == 2 ? (uint64_t)ce : lane == 3 ? (uint64_t)de : 0ull;
             if (ce) t_stop = t;
         }
         // ================= consensus: this step's deliveries in canonical (kp, s) order
@@ -634,7 +641,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        tot_msg += wave_sum(msg_now);
+        acc_add(0u, wave_sum(msg_now));
         msg_now = 0;
         // the step is consumed: its ring row is free for step t + RW
         if (lane < 2 * nkw) (lane < nkw ? s_dkA : s_dkB)[row * nkw + (lane % nkw)] = 0;
@@ -658,6 +665,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc
     }
 
     // ---- write back (result readers: inst, istats, items, cons0/cons1, gcount)
+    const uint64_t tot_msg = acc_get(0), tot_arr = acc_get(1), tot_cell = acc_get(2), tot_del = acc_get(3);
+    const uint64_t key_steps = acc_get(4);
     if (lane == 0) {
         gptr_t<uint64_t> ip = (gptr_t<uint64_t>)&gp(P.inst)[inst];
         *ip = (uint64_t)(status & 0xFFFF) | ((uint64_t)(t_stop & 0xFFFF) << 16) | ((uint64_t)(t & 0xFFFF) << 32);

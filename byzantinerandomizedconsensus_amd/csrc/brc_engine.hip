@@ -294,7 +294,7 @@ static int clear_state(Engine* e, bool full) {
     HIPCHK(e, hipMemsetAsync(e->cons1, 0, (size_t)e->nitems * e->lpi * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->hmask, 0, (size_t)e->nitems * e->cons_bytes, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount, 0, 8 * 8, e->stream));
-    HIPCHK(e, hipMemsetAsync(e->xsn, 0, (size_t)e->nitems * 4, e->stream));
+    if (!e->compact && !e->wide) HIPCHK(e, hipMemsetAsync(e->xsn, 0, (size_t)e->nitems * 4, e->stream));
     if (e->event_count) HIPCHK(e, hipMemsetAsync(e->event_count, 0, 8, e->stream));
     return BRC_OK;
 }
@@ -466,7 +466,9 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
         {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8 : 8},
-        {(void**)&e->xsend, (size_t)e->nitems * XSEND_MAX * 24}, {(void**)&e->xsn, (size_t)e->nitems * 4},
+        // extra-SEND records: the non-lean narrow kernels only (the lean and wide kernels refuse extra SENDs)
+        {(void**)&e->xsend, (e->compact || e->wide) ? 8 : (size_t)e->nitems * XSEND_MAX * 24},
+        {(void**)&e->xsn, (e->compact || e->wide) ? 8 : (size_t)e->nitems * 4},
     };
     for (auto& a : allocs)
         if (hipMalloc(a.p, std::max<size_t>(a.bytes, 8)) != hipSuccess) {

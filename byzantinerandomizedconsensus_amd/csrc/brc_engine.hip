@@ -179,9 +179,9 @@ struct Engine {
     // slot generation budget: reallocations of one key slot are bounded by max phase index / Q + 2
     // per epoch (brc_reset to brc_reset); gen_base sums the epochs since the last full clear
     uint64_t gen_base = 0, gen_cur = 0;
-    std::vector<std::pair<uint64_t, uint32_t>> send_keys;   // (instance, kp<<16|s) of injected SENDs
-    struct SendDst { uint64_t inst; uint32_t key, node; uint64_t dst; };
-    std::vector<SendDst> send_dst;               // ... and each sender's destinations (extra SENDs)
+    // injected SENDs per key (instance << 32 | kp << 16 | s): how many, and each sender's destinations
+    std::unordered_map<uint64_t, uint32_t> send_count;
+    std::unordered_map<uint64_t, std::vector<std::pair<uint32_t, uint64_t>>> send_dst;
     struct XRec { uint32_t k, t, seg; uint64_t smask, dst; };
     std::unordered_map<uint64_t, std::vector<XRec>> xrec;   // item -> extra-SEND records (P.xsend)
     // key-lifetime kernel (brc_life.h): eligible configuration, engine fresh since create / reset,
@@ -549,8 +549,8 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
     std::vector<uint64_t> reopen;
     std::vector<InjDev> staged;
     std::vector<uint64_t> staged_item;
-    std::vector<std::pair<uint64_t, uint32_t>> new_sends;
-    std::vector<Engine::SendDst> new_send_dst;
+    std::unordered_map<uint64_t, uint32_t> new_count;                                   // this batch's SENDs
+    std::unordered_map<uint64_t, std::vector<std::pair<uint32_t, uint64_t>>> new_dst;
     for (size_t i = 0; i < count; ++i) {
         const brc_injection& x = list[i];
         if (x.instance >= c.instances || x.node >= c.n || x.t > c.step_cap) { e->err = "injection out of range"; return BRC_E_INVALID; }
@@ -586,27 +586,30 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
                 // a second SEND of a key (another origin or the same, one payload string SENT again):
                 // an extra-SEND record on the non-lean step kernels; the lean and wide kernels model
                 // one SEND per key
-                auto key = std::make_pair(x.instance, (uint32_t)(x.kp * 0x10000u + x.s));
-                if ((e->compact || e->wide) &&
-                    (std::find(e->send_keys.begin(), e->send_keys.end(), key) != e->send_keys.end() ||
-                     std::find(new_sends.begin(), new_sends.end(), key) != new_sends.end())) {
+                const uint64_t k64 = (x.instance << 32) | (uint64_t)(x.kp * 0x10000u + x.s);
+                auto it0 = e->send_count.find(k64);
+                auto it1 = new_count.find(k64);
+                const uint32_t before = (it0 != e->send_count.end() ? it0->second : 0u) +
+                                        (it1 != new_count.end() ? it1->second : 0u);
+                if ((e->compact || e->wide) && before) {
                     e->err = "a key can be SENT only once on this kernel (n in 33..64 with sender peers, or n > 64)";
                     return BRC_E_UNSUPPORTED;
                 }
-                new_sends.push_back(key);
+                ++new_count[k64];
                 // this node's earlier SENDs of the key (this batch included): r.type = 1 marks a repeat
                 // (brc_step.h: a COPY event with connection peers); sender peers carry a repeated
                 // message on a link no further (the links it used are dropped from the record)
                 uint64_t prev = 0;
                 bool had = false;
-                for (const auto* v : {&e->send_dst, &new_send_dst})
-                    for (const auto& q : *v)
-                        if (q.inst == x.instance && q.key == key.second && q.node == x.node) { prev |= q.dst; had = true; }
-                new_send_dst.push_back({x.instance, key.second, x.node, r.dst});
+                for (const auto* mp : {&e->send_dst, &new_dst}) {
+                    auto it = mp->find(k64);
+                    if (it != mp->end())
+                        for (const auto& q : it->second)
+                            if (q.first == x.node) { prev |= q.second; had = true; }
+                }
+                new_dst[k64].push_back({x.node, r.dst});
                 // a key SENT before (by any node): an extra-SEND record (bit 1), bit 0 = this node's repeat
-                const bool again = !(e->compact || e->wide) &&
-                                   (std::find(e->send_keys.begin(), e->send_keys.end(), key) != e->send_keys.end() ||
-                                    std::count(new_sends.begin(), new_sends.end(), key) > 1);
+                const bool again = !(e->compact || e->wide) && before > 0;
                 r.type = (again ? 2 : 0) | (had ? 1 : 0);
                 if (c.peer_mode == BRC_PEER_SENDER) r.dst &= ~prev;
                 drop = had && r.dst == 0;
@@ -679,8 +682,11 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         HIPCHK(e, hipMemcpyAsync(e->xsn + kv.first, &xbuf[o + 3 * XSEND_MAX], 4, hipMemcpyHostToDevice, e->stream));
     }
     for (size_t i = 0; i < staged.size(); ++i) e->pending[staged_item[i]].push_back(staged[i]);
-    e->send_keys.insert(e->send_keys.end(), new_sends.begin(), new_sends.end());
-    e->send_dst.insert(e->send_dst.end(), new_send_dst.begin(), new_send_dst.end());
+    for (const auto& kv : new_count) e->send_count[kv.first] += kv.second;
+    for (auto& kv : new_dst) {
+        auto& v = e->send_dst[kv.first];
+        v.insert(v.end(), kv.second.begin(), kv.second.end());
+    }
     for (uint64_t in : reopen) {
         ist[in].status = BRC_RUNNING;
         HIPCHK(e, hipMemcpyAsync(&e->inst[in], &ist[in], sizeof(InstState), hipMemcpyHostToDevice, e->stream));
@@ -781,7 +787,7 @@ int brc_reset(void* h) {
     int rc = clear_state(e, full);   // full: gen_base = gen_cur = 0
     if (rc) return rc;
     for (auto& v : e->pending) v.clear();
-    e->send_keys.clear();
+    e->send_count.clear();
     e->send_dst.clear();
     e->xrec.clear();
     if (e->pattern_active) {

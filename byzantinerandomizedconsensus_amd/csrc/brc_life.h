@@ -56,8 +56,11 @@ constexpr uint32_t LIFE_NEVER = 0xFFFFu;         // relative send step: not sent
 __device__ __forceinline__ uint32_t lm_s1(uint32_t m) { return m & 0x3FFFu; }
 __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 
+#ifndef BRC_LIFE_PL_CONN_WAVES
+#define BRC_LIFE_PL_CONN_WAVES 6   // per-link form, connection peers: waves per SIMD (A/B: 5 284.4, 6 273.2, 7 277.5 ms)
+#endif
 template <int MODE, bool PL>
-__global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? 5 : 6) : 8) void brc_life(const Params* __restrict__ pp) {
+__global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAVES : 6) : 8) void brc_life(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     constexpr uint32_t RW = LIFE_RW;

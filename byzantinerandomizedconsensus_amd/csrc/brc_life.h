@@ -151,6 +151,12 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 #pragma unroll
         for (int i = 0; i < DL; ++i) OV[i] = uni64(seg_or<64, uint64_t>(honest ? L[i] : 0ull));
     }
+    // PL: this lane's delays to honest receivers as a sender (bit i: delay i+1), for the pending steps
+    uint32_t myout = 0;
+    if constexpr (PL) {
+#pragma unroll
+        for (int i = 0; i < DL; ++i) myout |= (uint32_t)((OV[i] >> lane) & 1ull) << i;
+    }
     // PL: this wave's delivery-bitmap ring in HBM, word (row, w) of this lane at [(row * nkw + w) * 64]
     uint64_t* const dring = PL ? P.dring + item * (uint64_t)RW * nkw * 64 + lane : nullptr;
 
@@ -476,11 +482,17 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             // the messages sent now land on fast receivers after 1 step (fast senders) and on every
             // other (sender, receiver) pair after Dd steps
             if (PL) {
-                // a message sent now lands after every delay i+1 some link of its sender has to an honest receiver
-#pragma unroll
-                for (int i = 0; i < DL; ++i) {
-                    if (eb & OV[i]) pendE |= rb << (i + 1);
-                    if (rbm & OV[i]) pendR |= rb << (i + 1);
+                // a message sent now lands after every delay i+1 some link of its sender has to an honest
+                // receiver: the senders' delay sets OR-ed over the wave (one DPP reduction, VALU)
+                if (eb | rbm) {
+                    uint32_t x = (es ? myout : 0u) | ((rs ? myout : 0u) << 8);
+                    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
+                    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
+                    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);
+                    x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);
+                    x = uni32(rl(x, 0) | rl(x, 16) | rl(x, 32) | rl(x, 48));
+                    pendE |= (uint64_t)(x & 0xFFu) << (r + 1);
+                    pendR |= (uint64_t)(x >> 8) << (r + 1);
                 }
             } else if (eb) {
                 if ((eb & Fm) && HF) pendE |= rb << 1;

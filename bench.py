@@ -12,15 +12,21 @@ reference's decide() upcall, core/byzantinerandomizedconsensus.py:94).  Instance
 independent, so ranks shard them (global Philox ids => results independent of N: weak
 scaling); the only collective is one RCCL all-reduce of the statistics.
 
-Two legs, one JSON line (rank 0):
+Legs, one JSON line (rank 0); each leg is one launch per step at 2^20 instances:
   reference  the protocol exactly as the reference runs it (quirks included) -- the headline
              `value`.  Its coin branch is dead, so split proposals decide "-1" in
              round 1; `decided_value_hist` shows that share.
   spec       the protocol the reference intends, with the common coin made reachable (SURVEY §8
              F3): "many coin rounds".  Its phase window Q = 8 doubles the key slots; with 4-B cells
-             2^20 instances still fit one engine (138 GB of cells), so it is one launch per step.
-             Larger counts run as tiles of an engine re-keyed per tile (brc_reset_at); the
-             statistics then come from one extra untimed pass.
+             2^20 instances still fit one engine (138 GB of cells).  Larger counts run as tiles of
+             an engine re-keyed per tile (brc_reset_at); the statistics then come from one extra
+             untimed pass.
+  conn       connection-identity peers (core/brbroadcast.py:69, what the shipped reference runs;
+             SURVEY §8 F1), slow-set delays: the key-lifetime kernel's two-class form.
+  connu      connection peers under per-link uniform[1,2] delays: its per-link form.
+  many       the reference protocol run to round cap 8 (SURVEY cfg4's "many rounds"): by round 8
+             ~1,000 keys of one instance are live at once (phase leakage), more than any cell store
+             holds at 2^20, so the engine runs it on the key-lifetime kernel (key window 32).
 """
 import argparse
 import json
@@ -37,6 +43,13 @@ CELL_BYTES = 4                                                  # lean kernels' 
 FLOOR_BYTES_PER_CELL_STEP = 2 * CELL_BYTES                      # this layout: the cell word read + written
 HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
 SPEC_TILE = 1 << 20                                             # SPEC (Q = 8) instances per engine tile
+MANY_CAP = 8                                                    # the many leg's round cap
+# leg -> (protocol mode, peer mode, delay model, delay max, key window)
+LEGS = {"reference": ("reference", "sender", "slowset", DELAY_MAX, 4),
+        "spec": ("spec", "sender", "slowset", DELAY_MAX, 8),
+        "conn": ("reference", "connection", "slowset", DELAY_MAX, 4),
+        "connu": ("reference", "connection", "uniform", 2, 4),
+        "many": ("reference", "sender", "slowset", DELAY_MAX, 32)}
 
 
 def parse():
@@ -45,12 +58,14 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
-    ap.add_argument("--legs", default="reference,spec,conn",
-                    help="comma list of reference (the headline value), spec (SURVEY §8 F3 coin rounds) and conn "
-                         "(connection-identity peers, what the shipped reference runs: SURVEY §8 F1)")
-    ap.add_argument("--mode", choices=("reference", "spec", "conn"), default=None,
+    ap.add_argument("--legs", default="reference,spec,conn,connu,many",
+                    help="comma list of reference (the headline value), spec (SURVEY §8 F3 coin rounds), conn "
+                         "(connection-identity peers, what the shipped reference runs: SURVEY §8 F1), connu (the same "
+                         "under per-link uniform[1,2] delays) and many (the reference protocol to round cap 8)")
+    ap.add_argument("--mode", choices=tuple(LEGS), default=None,
                     help="shorthand for --legs <mode> (the headline leg is the first one run)")
-    ap.add_argument("--round-cap", type=int, default=1)
+    ap.add_argument("--round-cap", type=int, default=1, help="round cap of every leg but many")
+    ap.add_argument("--many-cap", type=int, default=MANY_CAP, help="round cap of the many leg")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0: skip)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
@@ -64,21 +79,23 @@ def parse():
     return a
 
 
-def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
+def cpu_baseline(seconds, leg="reference", round_cap=1):
     """The C oracle (a scalar port of the reference's path) on the same workload, one thread per
     core (ctypes releases the GIL inside the C run): threads take interleaved global instance ids
     from 0 and run until `seconds` have passed.  Counters only (the oracle's light mode)."""
+    mode, peer, model, dmax, window = LEGS[leg]
     import concurrent.futures
     from oracle import oracle
     from tests.golden import specs as S
     threads = max(1, min(16, os.cpu_count() or 1))    # the GPU box's CPU share is 16
 
+    dm = {"slowset": 2, "uniform": 1}[model]
+
     def spec(g):
         if mode == "spec":
-            return S.spec_cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, g, round_cap=round_cap,
+            return S.spec_cons_spec(N_REPLICAS, F_FAULTS, SEED, dm, dmax, g, round_cap=round_cap,
                                     window=window, coin_seed=COIN_SEED)
-        return S.cons_spec(N_REPLICAS, F_FAULTS, SEED, 2, DELAY_MAX, g, round_cap=round_cap,
-                           peer_mode="connection" if mode == "conn" else "sender")
+        return S.cons_spec(N_REPLICAS, F_FAULTS, SEED, dm, dmax, g, round_cap=round_cap, peer_mode=peer)
 
     t0 = time.perf_counter()
 
@@ -103,12 +120,13 @@ def cpu_baseline(seconds, mode="reference", window=4, round_cap=1):
                       % (count, count - 1, dt, threads, arrivals / dt)}
 
 
-def load_profile(instances, kernel_ms, mode="reference"):
+def load_profile(instances, kernel_ms, mode="reference", cell_bytes=CELL_BYTES):
     """The committed rocprofv3 summary of this leg (profiles/pmc_traffic.json for the reference leg,
-    profiles/pmc_traffic_<mode>.json for the others, written by profiles/summarize.py): HBM bytes per
-    launch and the instruction-issue block.  Used only if it was taken on this workload and size and
-    its kernel time agrees with the live one within 15 % (the same kernel build); the agreement is
-    reported beside it."""
+    profiles/pmc_traffic_<leg>.json for the others, written by profiles/summarize.py): HBM bytes per
+    launch and the instruction-issue block.  Used only if it was taken on this workload, size and
+    kernel (cell_bytes: 4 for the step kernel's compact cells, 0 for the key-lifetime kernel, which
+    keeps no cells) and its kernel time agrees with the live one within 15 % (the same kernel
+    build); the agreement is reported beside it."""
     name = "pmc_traffic.json" if mode == "reference" else "pmc_traffic_%s.json" % mode
     path = os.path.join(ROOT, "profiles", name)
     try:
@@ -117,22 +135,23 @@ def load_profile(instances, kernel_ms, mode="reference"):
     except (OSError, ValueError):
         return None
     if d.get("instances") != instances or d.get("workload") != "cfg4" or not d.get("avg_ns") or \
-            d.get("mode", "reference") != mode or d.get("cell_bytes", 8) != CELL_BYTES:
+            d.get("mode", "reference") != mode or d.get("cell_bytes", 8) != cell_bytes:
         return None
     if abs(d["avg_ns"] / 1e6 - kernel_ms) > 0.15 * kernel_ms:
         return None
     return d
 
 
-def make_engine(mode, count, first, device, round_cap):
+def make_engine(leg, count, first, device, round_cap):
     from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd.engine import Engine
+    mode, peer, model, dmax, window = LEGS[leg]
     spec = mode == "spec"
     return Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
-                  delay_model=L.DELAY_SLOWSET, delay_max=DELAY_MAX, round_cap=round_cap, step_cap=4000,
-                  key_window=8 if spec else 4, variants=1, proposals=L.PROPOSALS_PHILOX,
+                  delay_model={"slowset": L.DELAY_SLOWSET, "uniform": L.DELAY_UNIFORM}[model], delay_max=dmax,
+                  round_cap=round_cap, step_cap=4000, key_window=window, variants=1, proposals=L.PROPOSALS_PHILOX,
                   instance_offset=first, device=device, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
-                  coin_seed=COIN_SEED, peer_mode=L.PEER_CONNECTION if mode == "conn" else L.PEER_SENDER)
+                  coin_seed=COIN_SEED, peer_mode=L.PEER_CONNECTION if peer == "connection" else L.PEER_SENDER)
 
 
 def collect(eng):
@@ -158,9 +177,10 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     from byzantinerandomizedconsensus_amd import shard
     per = args.instances
     first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
-    tile = count if mode == "reference" else min(count, SPEC_TILE)
+    tile = min(count, SPEC_TILE) if mode == "spec" else count
     tiles = [(first + o, min(tile, count - o)) for o in range(0, count, tile)]
-    eng = make_engine(mode, tiles[0][1], tiles[0][0], local, args.round_cap)
+    cap = args.many_cap if mode == "many" else args.round_cap
+    eng = make_engine(mode, tiles[0][1], tiles[0][0], local, cap)
 
     def barrier():
         if dist is not None:
@@ -213,21 +233,21 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     launches = len(tiles)
     cs_gpu = cell_steps / world
     secs = kernel_ms / 1e3
-    prof = load_profile(per, kernel_ms, mode) if launches == 1 else None
-    traffic = prof.get("hbm_bytes_per_launch") if prof else None
     if kernel not in ("step", "life"):
         raise SystemExit("%s leg: the launches ran different kernels (%s); its roofline cannot be priced" % (mode, kernel))
+    prof = load_profile(per, kernel_ms, mode, CELL_BYTES if kernel == "step" else 0) if launches == 1 else None
+    traffic = prof.get("hbm_bytes_per_launch") if prof else None
     if kernel == "life":
         # the key-lifetime kernel (csrc/brc_life.h) keeps a key's cells in registers for its whole
         # lifetime: no cell bytes move, HBM carries only the per-instance results
         roof = {"bound": "issue", "kernel": "brc_life", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": None, "traffic": traffic,
                 "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                "survey_model_frac": SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9 / HBM_PEAK_GBS,
-                "cell_steps_per_s": cs_gpu / secs, "cell_bytes": 0,
+                "survey_model_gbs": SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9,
+                "cell_steps_per_s": cs_gpu / secs, "cell_bytes": 0, "units_per_launch": cs_gpu / launches,
                 "note": "no HBM cell traffic (cells stay in registers for a key's lifetime): bound by instruction "
-                        "issue, not HBM; survey_model_frac prices SURVEY 8(d)'s %d B per cell-step"
-                        % SURVEY_BYTES_PER_CELL_STEP}
+                        "issue, not HBM; survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step (bytes this "
+                        "kernel never moves)" % SURVEY_BYTES_PER_CELL_STEP}
     else:
         # algorithmic bytes of THIS layout: the 4-B cell word read + written per cell-step
         achieved = FLOOR_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9
@@ -235,12 +255,12 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
         roof = {"bound": "hbm", "kernel": "brc_step", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
-                "survey_model_frac": survey / HBM_PEAK_GBS, "cell_bytes": CELL_BYTES,
+                "survey_model_gbs": survey, "cell_bytes": CELL_BYTES,
                 "bytes_per_unit": FLOOR_BYTES_PER_CELL_STEP, "units_per_launch": cs_gpu / launches,
                 "note": "achieved = %d B (the %d-B cell word read + written) x %d cell-steps per GPU per step (%d "
                         "launch%s) / kernel time; traffic = rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE per launch "
-                        "(profiles/pmc_traffic*.json); survey_model_frac prices SURVEY 8(d)'s %d B per cell-step, which "
-                        "credits n-bit ECHO/READY masks this design never moves, so it can pass 1"
+                        "(profiles/pmc_traffic*.json); survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step, which "
+                        "credits n-bit ECHO/READY masks this design never moves (so it can exceed the peak)"
                         % (FLOOR_BYTES_PER_CELL_STEP, CELL_BYTES, cs_gpu, launches, "" if launches == 1 else "es",
                            SURVEY_BYTES_PER_CELL_STEP)}
     if prof:
@@ -264,13 +284,20 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
                                       "decide_rounds_sum", "lane_loads", "max_t")},
         "roofline": roof,
         "kernel": kernel,
-        "workload": "cfg4: n=64 f=21 %s consensus to %s, slow-set delays D=8, %d instances/GPU"
-                    % ({"spec": "SPEC-protocol (common coin, phase window 8)",
-                        "conn": "reference-protocol, connection-identity peers (core/brbroadcast.py:69),"}.get(
-                        mode, "reference-protocol"),
-                       "first decision" if args.round_cap == 1 else "%d decisions" % args.round_cap, per),
+        "workload": workload_name(mode, cap, per),
+        "round_cap": cap,
     }
     return leg
+
+
+def workload_name(leg, cap, per):
+    proto, peer, model, dmax, window = LEGS[leg]
+    return "cfg4: n=64 f=21 %s consensus to %s, %s, %s peers, key window %d, %d instances/GPU" % (
+        "SPEC-protocol (common coin)" if proto == "spec" else "reference-protocol",
+        "first decision" if cap == 1 else "%d decisions" % cap,
+        "slow-set delays D=%d" % dmax if model == "slowset" else "per-link uniform[1,%d] delays" % dmax,
+        "connection-identity (core/brbroadcast.py:69)" if peer == "connection" else "sender-identity",
+        window, per)
 
 
 def main():
@@ -312,12 +339,12 @@ def main():
             "dtype": "u32",
             "data": "synthetic (Philox4x32-10 proposals and slow sets, seed 0x5EED0004)",
             "config": {"workload": head["workload"], "n": N_REPLICAS, "f": F_FAULTS,
-                       "instances_per_gpu": args.instances, "round_cap": args.round_cap,
+                       "instances_per_gpu": args.instances, "round_cap": head["round_cap"],
                        "round_cap_meaning": "an instance is done when every honest replica has decided this many "
                                             "times (the run stops at that decision, not a give-up bound)",
                        "mode": head_mode,
-                       "key_window": 8 if head_mode == "spec" else 4,
-                       "peer_mode": "connection" if head_mode == "conn" else "sender",
+                       "key_window": LEGS[head_mode][4],
+                       "peer_mode": LEGS[head_mode][1],
                        "parallelism": "instance-sharded x%d" % world},
             "collective": (dist.get_backend() + " all-reduce of the statistics") if dist is not None else None,
         }
@@ -328,8 +355,7 @@ def main():
             if mode != head_mode:
                 out[mode + "_leg"] = leg
     if rank == 0 and world == 1 and not args.no_cpu and args.cpu_seconds > 0:     # N = 1 only
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, head_mode, 8 if head_mode == "spec" else 4,
-                                           args.round_cap)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, head_mode, head["round_cap"])
     if rank == 0 and head_mode == "reference" and args.round_cap == 1:
         # the reference's own Python path cannot travel to the GPU box: its rate on this workload was
         # measured in the build container (tools/ref_cpu_rate.py) and is reported beside, not as, the baseline

@@ -187,6 +187,9 @@ struct Engine {
     // key-lifetime kernel (brc_life.h): eligible configuration, engine fresh since create / reset,
     // and whether the last run used it (its instances are then final: no re-opening injections)
     bool life_cfg = false, fresh = true, life_done = false, last_life = false;
+    // false: the step kernel cannot serve this engine (its cells would not fit, or a lean key window
+    // above 32): only the key-lifetime kernel runs, and the step kernel's key-slot arrays are not allocated
+    bool step_ok = true;
     bool cells_ready = false;                    // the step kernel's cell array (allocated on first use
                                                  // when the lifetime kernel may serve the engine)
     uint32_t life_lds = 0;
@@ -271,7 +274,9 @@ static int ensure_cells(Engine* e) {
 
 static int clear_state(Engine* e, bool full) {
     const size_t keys = (size_t)e->cfg.instances * e->NK;
-    if (full) {
+    if (!e->step_ok) {
+        // lifetime kernel only: it keeps key slots in LDS; no cells, key metadata or activity ring
+    } else if (full) {
         if (e->cells_ready) {
             const int rc = fill_cells(e);
             if (rc) return rc;
@@ -285,7 +290,8 @@ static int clear_state(Engine* e, bool full) {
                            (uint64_t)keys);
         HIPCHK(e, hipGetLastError());
     }
-    HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8, e->stream));
+    if (e->step_ok)
+        HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->actany, 0, (size_t)e->nitems * 4, e->stream));
     HIPCHK(e, hipMemsetAsync(e->items, 0, (size_t)e->nitems * sizeof(ItemState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->inst, 0, (size_t)e->cfg.instances * sizeof(InstState), e->stream));
@@ -381,10 +387,13 @@ int brc_create(const brc_config* cfg, void** out) {
         (c.peer_mode == BRC_PEER_CONNECTION && c.mode != BRC_MODE_REFERENCE) ||
         (c.protocol != BRC_PROTO_BRB && c.protocol != BRC_PROTO_CONSENSUS) || c.delay_model > BRC_DELAY_GEOMETRIC ||
         (c.delay_model == BRC_DELAY_CONST && (c.delay_const < 1 || c.delay_const > c.delay_max)) ||
-        !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8 || c.key_window == 16 || c.key_window == 32) ||
+        !(c.key_window == 2 || c.key_window == 4 || c.key_window == 8 || c.key_window == 16 || c.key_window == 32 ||
+          c.key_window == 64 || c.key_window == 128) ||
         !(c.variants == 1 || c.variants == 2 || c.variants == 4) ||
         // more than 8 live phase indices per origin: reference / best-effort protocols on the narrow kernels
-        c.key_window * c.variants > ((c.mode != BRC_MODE_SPEC && c.n <= 64) ? 32u : 8u) ||
+        // (up to 128: the reference protocol's many-round runs; the lean kernels take <= 32 and
+        // leave larger windows to the key-lifetime kernel, below)
+        c.key_window * c.variants > ((c.mode != BRC_MODE_SPEC && c.n <= 64) ? 128u : 8u) ||
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
         c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB ||
@@ -428,19 +437,42 @@ int brc_create(const brc_config* cfg, void** out) {
     // log, no Byzantine pattern.  BRC_KERNEL=step | life | auto (default): auto runs connection-identity
     // peers on it (their step-kernel cells are 5 words); sender peers stay on the step kernel, which is
     // faster there
+    // The lifetime kernel keeps no cells, so it also runs sender peers whose step-kernel cell store
+    // would not fit in the free device memory (the reference protocol's many-round runs: its phase
+    // leakage keeps ~1,000 keys of one instance live by round 8 at n = 64) and the key
+    // windows above 32 the lean step kernel does not take.
     {
         const char* kv = getenv("BRC_KERNEL");
         const bool force_step = kv && strcmp(kv, "step") == 0, force_life = kv && strcmp(kv, "life") == 0;
         e->life_lds = lds_bytes_life(e->NK, e->nkw, spec, c.key_window, c.variants);
+        e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
         const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
                               c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
-                              c.delay_max <= 8 && e->life_lds <= 64 * 1024;
-        e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION);
-        e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
+                              c.delay_max <= 8 && e->life_lds <= 160 * 1024 &&
+                              // per-link form: its HBM delivery ring is [RW][NK] bits per instance
+                              !(e->life_pl && c.key_window * c.variants > 32);
+        bool big = e->compact && c.key_window * c.variants > 32;          // the lean kernels take <= 32
+        if (!big && e->compact && c.peer_mode == BRC_PEER_SENDER && hipSetDevice(c.device) == hipSuccess) {
+            size_t fr = 0, tot = 0;
+            const size_t cells = (size_t)e->nitems * (e->NK + 1) * 64 * 4;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && cells > fr / 10 * 9) big = true;
+            (void)hipGetLastError();
+        }
+        e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION || big);
+        e->step_ok = !big;
+        if (big && !e->life_cfg) {
+            g_create_err = c.key_window * c.variants > 32
+                ? "key windows above 32 at n in 33..64 with sender peers run on the key-lifetime kernel only "
+                  "(consensus, Philox / loaded proposals, delay_max <= 8, constant / slow-set delays, no event log)"
+                : "the step kernel's cells do not fit in free device memory and the key-lifetime kernel cannot run "
+                  "this configuration";
+            delete e;
+            return BRC_E_INVALID;
+        }
     }
     // narrow kernels: one lane clears one word of a ring row (act_types words per key word)
-    if ((e->wide ? e->nkw > (uint32_t)e->nkw_t : e->nkw * act_types(e->compact) > 64) || e->nitems > 0x7FFFFFFFull * WPB ||
-        e->lds_bytes > 160 * 1024) {
+    if ((e->step_ok && ((e->wide ? e->nkw > (uint32_t)e->nkw_t : e->nkw * act_types(e->compact) > 64) ||
+                        e->lds_bytes > 160 * 1024)) || e->nitems > 0x7FFFFFFFull * WPB) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
         delete e;
         return BRC_E_INVALID;
@@ -454,17 +486,18 @@ int brc_create(const brc_config* cfg, void** out) {
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return fail(BRC_E_HIP);
     if (hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) return fail(BRC_E_HIP);
     const size_t cells = (size_t)e->nitems * e->rows * e->lpi;
-    const size_t keys = (size_t)c.instances * e->NK;
+    const size_t keys = e->step_ok ? (size_t)c.instances * e->NK : 1;    // the step kernel's key-slot arrays
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, e->life_cfg ? 8 : cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
-        {(void**)&e->kdst, keys * 8 * e->bw}, {(void**)&e->act, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8},
+        {(void**)&e->kdst, keys * 8 * e->bw},
+        {(void**)&e->act, e->step_ok ? (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8 : 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},
         {&e->hmask, (size_t)e->nitems * e->cons_bytes}, {(void**)&e->inj_off, (size_t)e->nitems * 4},
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
-        {(void**)&e->dbits, (e->compact && spec) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
+        {(void**)&e->dbits, (e->compact && spec && e->step_ok) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
         {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8 : 8},
         // extra-SEND records: the non-lean narrow kernels only (the lean and wide kernels refuse extra SENDs)
         {(void**)&e->xsend, (e->compact || e->wide) ? 8 : (size_t)e->nitems * XSEND_MAX * 24},
@@ -482,7 +515,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->cells_ready = !e->life_cfg;
     if (hipMemsetAsync(e->inj_off, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
-    if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);
+    if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);   // keys = 1: 8 B
     // the lifetime kernel leaves its bitmap ring zero at exit
     if (e->life_cfg && e->life_pl &&
         hipMemsetAsync(e->dring, 0, (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8, e->stream) != hipSuccess)
@@ -627,37 +660,44 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         }
         const uint64_t item = x.instance / e->ipw;
         if (its[item].initialized != 0 && x.t < its[item].t) { e->err = "injection time is before the instance's current step"; return BRC_E_STATE; }
+        if (drop) continue;                      // carried on no link: changes no instance state
         if (ist[x.instance].status == BRC_QUIESCENT && e->life_done) {
             e->err = "instance finished by the key-lifetime kernel (no step state to resume): brc_reset first";
             return BRC_E_STATE;
         }
         if (ist[x.instance].status == BRC_QUIESCENT) reopen.push_back(x.instance);
         else if (ist[x.instance].status != BRC_RUNNING) { e->err = "instance already stopped"; return BRC_E_STATE; }
-        if (drop) continue;
         staged.push_back(r);
         staged_item.push_back(item);
     }
     // extra-SEND records (r.type bit 1) into their items' tables: a record of the same key, step and
-    // destinations without this sender takes it, else one whose arrivals all lie in steps already run,
-    // else a new one; all-or-nothing (a batch that overflows a table changes nothing)
+    // destinations without this sender takes it, else a new one (records whose arrivals all lie in
+    // steps already run leave the table when it is rewritten); all-or-nothing (a batch that
+    // overflows a table changes nothing)
     std::unordered_map<uint64_t, std::vector<Engine::XRec>> xnew;
     for (size_t i = 0; i < staged.size(); ++i) {
         const InjDev& r = staged[i];
         if (r.kind != BRC_INJ_SEND || !(r.type & 2)) continue;
         const uint64_t item = staged_item[i];
-        if (!xnew.count(item)) xnew[item] = e->xrec.count(item) ? e->xrec[item] : std::vector<Engine::XRec>();
+        if (!xnew.count(item)) {
+            // the table is rewritten: records whose arrivals all lie in steps already run are
+            // dropped, so the kernel's per-step scan covers live records only (xs_n shrinks)
+            std::vector<Engine::XRec> v0;
+            if (e->xrec.count(item))
+                for (const auto& q : e->xrec[item])
+                    if (!(its[item].initialized != 0 && q.t + c.delay_max < its[item].t)) v0.push_back(q);
+            xnew[item] = v0;
+        }
         auto& v = xnew[item];
-        int slot = -1, dead = -1;
+        int slot = -1;
         for (size_t j = 0; j < v.size(); ++j) {
             if (v[j].k == r.slot && v[j].t == r.t && v[j].seg == r.seg && v[j].dst == r.dst && !((v[j].smask >> r.node) & 1ull)) {
                 slot = (int)j;
                 break;
             }
-            if (dead < 0 && v[j].t + c.delay_max < its[item].t) dead = (int)j;
         }
         const Engine::XRec nr = {r.slot, r.t, r.seg, 1ull << r.node, r.dst};
         if (slot >= 0) v[slot].smask |= 1ull << r.node;
-        else if (dead >= 0) v[dead] = nr;
         else if (v.size() < XSEND_MAX) v.push_back(nr);
         else {
             e->err = "more than " + std::to_string(XSEND_MAX) + " extra-SEND records in flight in one item";
@@ -721,6 +761,12 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     bool no_inj = true;
     for (const auto& v : e->pending) if (!v.empty()) { no_inj = false; break; }
     const bool life = e->life_cfg && e->fresh && no_inj && max_steps == 0 && !e->values_wide;
+    if (!life && !e->step_ok) {
+        e->err = "this engine runs on the key-lifetime kernel only (its step-kernel state does not fit, or a key "
+                 "window above 32 at n in 33..64 with sender peers): a fresh run to completion, no injections, "
+                 "max_steps = 0, value ids < 4 (brc_reset first)";
+        return BRC_E_UNSUPPORTED;
+    }
     if (!life) {
         rc = ensure_cells(e);
         if (rc) return rc;

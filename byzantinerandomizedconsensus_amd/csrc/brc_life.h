@@ -191,7 +191,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     const bool cons_lane = honest;                 // consensus protocol (host-checked)
     uint32_t round = 0, phase = 0, nvals = 0, order = 0, vcount = 0;
     uint32_t dcount = 0, frnd = 0, ft = 0, fval = 0, lval = 0;
-    uint32_t clr = 0;                              // this lane's key slots created this step (bit s mod Q)
+    // this lane's keys created this step: phase indices clr_s .. clr_s + clr_n - 1 (a replica's SENDs of
+    // one step have consecutive indices: each phase end advances the index by one)
+    uint32_t clr_s = 0, clr_n = 0;
     uint32_t msg_now = 0;                          // SEND messages sent this step (per lane, counted at once)
 
     // honest origin d broadcasts SEND for its key (d, s) with value v (core/byzantinerandomizedconsensus.py:48-50,
@@ -201,7 +203,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t m = s_meta[k];
         if ((lm_s1(m) != 0 && t < lm_tend(m)) || s >= 0x3FFEu) { ovf = true; return; }
         s_meta[k] = ((t + 1u) << 16) | ((v & 3u) << 14) | (s + 1u);   // busy until simulated
-        clr |= 1u << (s & Qm);
+        if (clr_n == 0) clr_s = s;
+        ++clr_n;
         msg_now += n;
         st_smax = max(st_smax, s);
     };
@@ -517,17 +520,19 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         }
         if (lane == 0) s_meta[k] = (s_meta[k] & 0xFFFFu) | (last << 16);
     };
-    // the keys created this step (clr bits of every lane), each simulated once
+    // the keys created this step (every lane's clr_s .. clr_s + clr_n - 1), each simulated once
     auto simulate_new = [&]() {
-        for (uint64_t b = __ballot(clr != 0); b; b &= b - 1) {
+        for (uint64_t b = __ballot(clr_n != 0); b; b &= b - 1) {
             const int L = __ffsll((unsigned long long)b) - 1;
-            for (uint32_t cm = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr, L)); cm; cm &= cm - 1) {
-                const uint32_t k = ((uint32_t)L * NV) * Q + (uint32_t)__ffs(cm) - 1u;
+            const uint32_t s0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_s, L));
+            const uint32_t cn = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_n, L));
+            for (uint32_t i = 0; i < cn; ++i) {
+                const uint32_t k = ((uint32_t)L * NV) * Q + ((s0 + i) & Qm);
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 simulate(k);
             }
         }
-        clr = 0;
+        clr_n = 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     };
 
@@ -565,8 +570,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         // ================= consensus: this step's deliveries in canonical (kp, s) order
         for (uint32_t i = lane; i < NK; i += 64) s_snap[i] = (uint16_t)s_meta[i];
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll 1
-        for (uint32_t w = 0; w < nkw; ++w) {
+        // this step's delivery bits of key word w for this lane (read once: PL clears the ring word)
+        auto dword = [&](uint32_t w) -> uint64_t {
             uint64_t bits;
             if constexpr (PL) {
                 uint64_t* const dp = dring + (row * nkw + w) * 64;
@@ -577,6 +582,33 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 const uint64_t kA = s_dkA[row * nkw + w], kB = s_dkB[row * nkw + w];
                 bits = cons_lane ? (laneF ? kA : kB) : 0ull;
             }
+            return bits;
+        };
+        if (Q >= 64) {
+            // key windows of 64 / 128 (the reference protocol's many-round runs): a key prefix
+            // (origin, variant) spans Q / 64 whole words; its deliveries of one step (one origin) go one
+            // at a time, smallest phase index first -- the canonical (kp, s) order
+            const uint32_t wpg = Q > 64 ? Q / 64 : 1u;
+#pragma unroll 1
+            for (uint32_t w = 0; w < nkw; w += wpg) {
+                uint64_t gb[2] = {dword(w), wpg > 1 ? dword(w + 1) : 0ull};
+                while (gb[0] | gb[1]) {
+                    uint32_t bs = 0xFFFFFFFFu, bk = 0;
+                    for (uint32_t j = 0; j < wpg; ++j)
+                        for (uint64_t x = gb[j]; x; x &= x - 1) {
+                            const uint32_t kk = (w + j) * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1u;
+                            const uint32_t s1 = s_snap[kk] & 0x3FFFu;
+                            if (s1 < bs) { bs = s1; bk = kk; }
+                        }
+                    gb[(bk >> 6) - w] &= ~(1ull << (bk & 63));
+                    if constexpr (SPEC) spec_deliver(bk);
+                    else cons_deliver_vh((uint32_t)s_snap[bk] >> 14, bk >> ksh);
+                }
+            }
+        } else
+#pragma unroll 1
+        for (uint32_t w = 0; w < nkw; ++w) {
+            uint64_t bits = dword(w);
             if constexpr (SPEC) {
                 // word at once when every delivering lane is at one phase index c0 and its current-phase
                 // deliveries cannot complete the phase (brc_step.h, SPEC consensus pass)
@@ -659,7 +691,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         acc_add(0u, wave_sum(msg_now));
         msg_now = 0;
         // the step is consumed: its ring row is free for step t + RW
-        if (lane < 2 * nkw) (lane < nkw ? s_dkA : s_dkB)[row * nkw + (lane % nkw)] = 0;
+        for (uint32_t i = lane; i < 2 * nkw; i += 64) (i < nkw ? s_dkA : s_dkB)[row * nkw + (i % nkw)] = 0;
         if (lane == row) { rg_arr = 0; rg_msg = 0; rg_cell = 0; rg_del = 0; }
         rows &= ~(1u << row);
         // ================= per-instance stop conditions (brc_step.h)

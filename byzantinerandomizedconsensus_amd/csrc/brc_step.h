@@ -1804,6 +1804,31 @@ void brc_step(const Params* __restrict__ pp) {
         {
             const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
             const bool cons = P.protocol == BRC_PROTO_CONSENSUS && honest && running;
+            if (!LEAN && !SPEC && Q >= 64) {
+                // key windows of 64 / 128 (the reference protocol's many-round runs; brc_create
+                // keeps the lean and SPEC kernels at <= 32): a key prefix spans Q / 64 whole words; its
+                // deliveries of one step go one at a time, smallest phase index first (canonical (kp, s))
+                const uint32_t wpg = Q > 64 ? Q / 64 : 1u;
+#pragma unroll 1
+                for (uint32_t w = 0; w < nkw; w += wpg) {
+                    uint64_t gb[2] = {0ull, 0ull};
+                    for (uint32_t j = 0; j < wpg; ++j) {
+                        gb[j] = cons ? s_dbits[(w + j) * 64 + lane] : 0ull;
+                        s_dbits[(w + j) * 64 + lane] = 0;
+                    }
+                    while (gb[0] | gb[1]) {
+                        uint32_t bs = 0xFFFFFFFFu, bk = 0;
+                        for (uint32_t j = 0; j < wpg; ++j)
+                            for (uint64_t x = gb[j]; x; x &= x - 1) {
+                                const uint32_t kk = (w + j) * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1u;
+                                const uint32_t s1 = m_s1(s_meta[mbase + kk]);
+                                if (s1 < bs) { bs = s1; bk = kk; }
+                            }
+                        gb[(bk >> 6) - w] &= ~(1ull << (bk & 63));
+                        cons_deliver(bk);
+                    }
+                }
+            } else
 #pragma unroll 1
             for (uint32_t w = 0; w < nkw; ++w) {
                 uint64_t bits;

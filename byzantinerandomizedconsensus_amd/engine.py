@@ -147,6 +147,21 @@ class Engine:
                         for d in range(self.n)])
         return out
 
+    def instances_array(self, first=0, count=None):
+        """instances_result() as one numpy structured array (brc_instance_result fields, status as
+        its numeric code): the bulk read for batches of millions of instances."""
+        count = self.instances - first if count is None else count
+        arr = (L.InstanceResult * count)()
+        self._chk(self._lib.brc_read_instances(self._h, first, count, arr))
+        return np.ctypeslib.as_array(arr).copy()
+
+    def replicas_array(self, first=0, count=None):
+        """replicas() as one numpy structured array of shape [count, n] (brc_replica_result fields)."""
+        count = self.instances - first if count is None else count
+        arr = (L.ReplicaResult * (count * self.n))()
+        self._chk(self._lib.brc_read_replicas(self._h, first, count, arr))
+        return np.ctypeslib.as_array(arr).reshape(count, self.n).copy()
+
     def events(self):
         """Event log: (instance, t, kind, node, type, a, b, value id) tuples, in device order."""
         cnt = ctypes.c_size_t(0)

@@ -26,9 +26,11 @@ Deviations from the reference, all reported by exceptions and never silent:
   two-bit ids.
 * A payload SENT by two different origins (or SENT again) is one key in the reference (its
   dicts are keyed by the payload string); the engine models it as one key with extra SENDs
-  (brc_step.h extra-SEND records, up to 8 in flight) on clusters up to 32 nodes and with
-  connection peers up to 64; on the others (33..64 nodes with sender peers, more than 64) it
-  raises ``EngineError``.
+  (brc_step.h extra-SEND records: up to 16 per wave item, shared by the instances packed into
+  it) on clusters up to 32 nodes and with connection peers up to 64; on the others (33..64
+  nodes with sender peers, more than 64) a second origin raises ``EngineError``.  A node that
+  SENDs its own payload again with sender peers is a no-op everywhere: the network drops a
+  duplicate on every link (tests/golden/refharness.py).
 * ``broadcast(type, m)`` takes SEND, ECHO and READY (the reference also puts other types on
   the wire, which its handler then ignores): other types raise ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
@@ -236,6 +238,9 @@ class Cluster:
             raise L.EngineError(L.E_UNSUPPORTED, "raw BRB SENDs on a consensus cluster")
         payload = str(payload)
         key = self._key_of(i, payload)
+        sender_peers = self.beb or self.cfg["peer_mode"] == "sender"
+        if key[0] == i and key in self.sent and sender_peers and self.lean_or_wide:
+            return            # the same node's repeat: a duplicate on every link, nothing travels
         if (key[0] != i or key in self.sent) and self.lean_or_wide:
             raise L.EngineError(L.E_UNSUPPORTED, "payload %r SENT twice (one reference key) on a %d-node cluster "
                                 "with %s peers" % (payload, len(self.peers), self.cfg["peer_mode"]))

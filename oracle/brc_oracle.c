@@ -482,6 +482,7 @@ int oracle_run(const oracle_spec* sp, oracle_result* res) {
     S->sp = sp; S->res = res; S->n = sp->n; S->f = sp->f; S->D = sp->dmax;
     res->status = 0; res->t_stop = 0; res->msgs_sent = 0; res->arrivals = 0;
     res->n_deliver = res->n_decide = res->n_send = 0;
+    res->cell_steps = 0;
     for (uint32_t s = 0; s < S->n; ++s)
         for (uint32_t d = 0; d < S->n; ++d)
             S->delay[s][d] = (uint8_t)oracle_delay(sp->n, sp->f, sp->seed, sp->delay_model, sp->dmax,
@@ -508,6 +509,9 @@ int oracle_run(const oracle_spec* sp, oracle_result* res) {
         msg_t* v = b->v; size_t cnt = b->n;
         b->v = NULL; b->n = 0; b->cap = 0;
         qsort(v, cnt, sizeof(msg_t), msg_cmp);
+        /* cell-steps: distinct (receiver, key) among the step's messages (sorted by dst, kp, s) */
+        for (size_t i = 0; i < cnt; ++i)
+            if (i == 0 || v[i].dst != v[i - 1].dst || v[i].key != v[i - 1].key) res->cell_steps++;
         const int spec = sp->mode == OR_MODE_SPEC || sp->mode == OR_MODE_SPEC_BRB;
         const int beb = sp->mode == OR_MODE_BEB || sp->mode == OR_MODE_BEB_CONSENSUS;
         for (size_t i = 0; i < cnt && !S->err; ++i) {

@@ -40,7 +40,7 @@ class _Result(ctypes.Structure):
                 ("decide", ctypes.POINTER(ctypes.c_uint32)), ("decide_cap", ctypes.c_size_t),
                 ("n_decide", ctypes.c_size_t),
                 ("sends", ctypes.POINTER(ctypes.c_uint32)), ("send_cap", ctypes.c_size_t),
-                ("n_send", ctypes.c_size_t)]
+                ("n_send", ctypes.c_size_t), ("cell_steps", ctypes.c_uint64)]
 
 
 _lib = None
@@ -101,9 +101,10 @@ def expand_actions(actions, n):
     return out
 
 
-def run(spec, light=False):
+def run(spec, light=False, kinds=("deliver", "decide", "send")):
     """Run one instance of ``spec`` (harness format) and return the harness result format.
-    ``light``: status and counters only (no event lists; one C call, no Python conversion)."""
+    ``light``: status and counters only (no event lists; one C call, no Python conversion).
+    ``kinds``: the event lists to return (the others come back empty; their counts are exact)."""
     acts = expand_actions(spec.get("actions", []), spec["n"])
     arr = (_Action * max(1, len(acts)))()
     for i, a in enumerate(acts):
@@ -123,31 +124,33 @@ def run(spec, light=False):
                g=spec["g"], step_cap=spec.get("step_cap", 10000), n_actions=len(acts),
                byz=_mask4(byz), actions=arr, coin_seed=spec.get("coin_seed", 0), window=spec.get("window", 0),
                peer_mode=PEER_MODES[spec.get("peer_mode", "sender")])
-    cap = 0 if light else 4096
+    names = ("deliver", "decide", "send")
+    caps = [0 if light or k not in kinds else 65536 for k in names]
     while True:
-        bufs = [(ctypes.c_uint32 * (cap * w))() for w in (4, 4, 5)]
-        res = _Result(deliver=bufs[0], deliver_cap=cap, decide=bufs[1], decide_cap=cap,
-                      sends=bufs[2], send_cap=cap)
+        bufs = [(ctypes.c_uint32 * (c * w))() for c, w in zip(caps, (4, 4, 5))]
+        res = _Result(deliver=bufs[0], deliver_cap=caps[0], decide=bufs[1], decide_cap=caps[1],
+                      sends=bufs[2], send_cap=caps[2])
         rc = lib().oracle_run(ctypes.byref(sp), ctypes.byref(res))
         if rc != 0:
             raise RuntimeError("oracle_run failed: %d" % rc)
-        if light or max(res.n_deliver, res.n_decide, res.n_send) <= cap:
+        got = (res.n_deliver, res.n_decide, res.n_send)
+        if light or all(k not in kinds or n <= c for k, n, c in zip(names, got, caps)):
             break
-        cap = 2 * max(res.n_deliver, res.n_decide, res.n_send)
+        caps = [2 * n if k in kinds and n > c else c for k, n, c in zip(names, got, caps)]
 
     if light:
         return {"status": STATUS.get(res.status), "t_stop": res.t_stop, "msgs_sent": res.msgs_sent,
-                "arrivals": res.arrivals,
+                "arrivals": res.arrivals, "cell_steps": res.cell_steps,
                 "counts": {"deliver": res.n_deliver, "decide": res.n_decide, "send": res.n_send}}
 
-    def rows(buf, cnt, w):
-        return [list(buf[i * w:(i + 1) * w]) for i in range(cnt)]
+    def rows(buf, cnt, w, k):
+        return [list(buf[i * w:(i + 1) * w]) for i in range(cnt)] if k in kinds else []
 
-    dec = rows(bufs[1], res.n_decide, 4)
+    dec = rows(bufs[1], res.n_decide, 4, "decide")
     values = spec.get("values")
     if values is not None:
         dec = [[t, nd, r, values[v]] for t, nd, r, v in dec]
     return {"status": STATUS.get(res.status), "t_stop": res.t_stop, "msgs_sent": res.msgs_sent,
-            "arrivals": res.arrivals,
-            "events": {"deliver": rows(bufs[0], res.n_deliver, 4), "decide": dec,
-                       "send": rows(bufs[2], res.n_send, 5)}}
+            "arrivals": res.arrivals, "cell_steps": res.cell_steps,
+            "events": {"deliver": rows(bufs[0], res.n_deliver, 4, "deliver"), "decide": dec,
+                       "send": rows(bufs[2], res.n_send, 5, "send")}}

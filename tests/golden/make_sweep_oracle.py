@@ -39,7 +39,7 @@ def one(job):
     for t, node, rnd, val in sorted(r["events"]["decide"]):
         first.setdefault(node, [rnd, t, val])
     return {"f": f, "g": g, "status": r["status"], "t_stop": r["t_stop"], "msgs_sent": r["msgs_sent"],
-            "arrivals": r["arrivals"], "first_decide": [first.get(d) for d in range(N)]}
+            "arrivals": r["arrivals"], "cell_steps": r["cell_steps"], "first_decide": [first.get(d) for d in range(N)]}
 
 
 def main():

@@ -277,6 +277,10 @@ def scenario_groups():
     # to 13 phase indices of one origin in flight by round 8 (key_window: the engine window to use)
     G["cons_slowset_n16_r8"] = [dict(cons_spec(16, 5, 0x5EED0004, 2, 8, g, round_cap=8), key_window=16)
                                 for g in range(3)]
+    # SURVEY cfg4's round cap 64 (at n = 16): by round 64 up to 99 phase indices of one origin are in
+    # flight (oracle-measured), so the engine runs it with a key window of 128
+    G["cons_slowset_n16_r64"] = [dict(cons_spec(16, 5, 0x5EED0004, 2, 8, g, round_cap=64), key_window=128)
+                                 for g in range(2)]
     G["cons_slowset_n64"] = [cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=1) for g in range(1)]
     # large committees (the wide kernel, n > 64)
     G["brb_uniform_n100"] = [brb_spec(100, 33, 0x5EED0005, 1, 4, g, [(0, 0, 0), (0, 57, 0), (3, 99, 0), (5, 0, 1)])

@@ -19,6 +19,18 @@ def groups():
     return out
 
 
+_CELL_STEPS = None
+
+
+def cell_steps(group, idx):
+    """The oracle's cell-step count of fixture case (group, idx) (tests/golden/make_cell_steps.py)."""
+    global _CELL_STEPS
+    if _CELL_STEPS is None:
+        with open(os.path.join(GOLDEN, "oracle_cell_steps.json")) as fh:
+            _CELL_STEPS = json.load(fh)["cases"]
+    return _CELL_STEPS[group][idx]
+
+
 def digest(rows):
     return hashlib.sha256(json.dumps(rows, separators=(",", ":")).encode()).hexdigest()
 

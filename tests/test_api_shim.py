@@ -174,6 +174,35 @@ def test_cluster_value_table_width():
         network.reset()
 
 
+def test_repeat_send_on_lean_cluster():
+    """33..64 nodes with sender peers (the lean kernel: one SEND per key): a node SENDing its own
+    payload again is a duplicate on every link -- the reference network carries nothing
+    (tests/golden/refharness.py) -- so it is a no-op; a second origin of the payload is refused."""
+    from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
+    network.reset()
+    try:
+        network.configure(peer_mode="sender")
+        peers = _peers(40, 7100)
+        nodes = [BRBroadcast(40, 13, p, peers, None) for p in peers]
+        nodes[5].broadcast(BRBroadcast.SEND, "A")
+        nodes[5].broadcast(BRBroadcast.SEND, "A")        # the same node again: dropped on every link
+        c = nodes[0].cluster
+        assert [(a["node"], a["kp"], a["s"]) for a in c.actions] == [(5, 5, 0)]
+        with pytest.raises(L.EngineError):
+            nodes[6].broadcast(BRBroadcast.SEND, "A")    # a second origin: one key, two SENDs
+        assert len(c.actions) == 1
+        network.reset()
+        network.configure(peer_mode="connection")        # connection peers: a repeat travels again
+        peers = _peers(70, 7200)
+        nodes = [BRBroadcast(70, 23, p, peers, None) for p in peers]
+        nodes[5].broadcast(BRBroadcast.SEND, "A")
+        with pytest.raises(L.EngineError):
+            nodes[5].broadcast(BRBroadcast.SEND, "A")    # the wide kernel models one SEND per key
+    finally:
+        network.configure(peer_mode="connection")
+        network.reset()
+
+
 def test_step_event_order():
     evs = [(L.EV_DELIVER, 2, 0, 0), (L.EV_DELIVER, 0, 3, 0), (L.EV_DELIVER, 0, 1, 1), (L.EV_DELIVER, 0, 1, 0)]
     assert network.order_step_events(evs) == [(1, 0, 1, 0), (1, 0, 1, 1), (1, 0, 3, 0), (1, 2, 0, 0)]

@@ -34,7 +34,7 @@ def _L():
     return L
 
 
-KEYS = ("status", "t_stop", "msgs_sent", "arrivals")
+KEYS = ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps")   # cell_steps: the roofline unit
 
 
 def _run(kw, first, count, ids=()):
@@ -225,42 +225,85 @@ def test_cfg4_bench_batch_2p20_sampled(mode):
         assert vals["-1"] == N * 64, vals
 
 
-@pytest.mark.parametrize("mode", ["reference", "spec"])
-def test_cfg4_long_consensus_many_rounds(mode):
-    """Long-running consensus at scale (the reference re-proposes forever,
-    core/byzantinerandomizedconsensus.py:96-106): 2^17 n=64 f=21 instances of the cfg4 slow-set
-    schedule (D = 8) run to round_cap = 8 decisions per replica, so slots recycle and the compact
-    cells' epoch moves across many rounds under a full batch.  The reference protocol's phase
-    leakage (:57-61, :71-78: deliveries of any phase count toward the current one) lets fast
-    replicas run ahead, so up to 17 phase indices of one origin are in flight by round 8: it runs
-    with a key window of 32 (SPEC needs 8).  Sampled instances equal the oracle (counters and every
-    replica's first and last decision, values included)."""
-    L = _L()
-    N, CAP = 1 << 17, 8
-    spec = mode == "spec"
-    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
-              round_cap=CAP, step_cap=4000, key_window=8 if spec else 32, proposals=L.PROPOSALS_PHILOX,
-              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
-    ids = sorted(random.Random(8).sample(range(N), 6)) + [N - 1]
-    with _engine(instance_offset=0, instances=N, **kw) as eng:
-        eng.run()
-        res_all = eng.instances_result()
-        res = {i: res_all[i] for i in ids}
-        reps = {i: eng.replicas(i, 1)[0] for i in ids}
-    assert all(r["status"] == "done" for r in res_all)      # no BRC_OVERFLOW
-    for g in ids:
-        if spec:
-            exp = oracle.run(S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8,
-                                              coin_seed=0xC017C017))
-        else:
-            exp = oracle.run(S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP))
-        for k in KEYS:
-            assert res[g][k] == exp[k], (g, k)
+def _oracle_first_last(specs):
+    """The oracle on several specs at once (threads: ctypes releases the GIL in the C run): per
+    spec the result and every replica's (first decision, last value, decide count)."""
+    import concurrent.futures
+    with concurrent.futures.ThreadPoolExecutor(min(8, len(specs))) as ex:
+        outs = list(ex.map(lambda sp: oracle.run(sp, kinds=("decide",)), specs))
+    per = []
+    for exp in outs:
         first, last, count = {}, {}, {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):
             first.setdefault(node, (rnd, t, VID[val]))
             last[node] = VID[val]
             count[node] = count.get(node, 0) + 1
+        per.append((exp, first, last, count))
+    return per
+
+
+@pytest.mark.parametrize("mode", ["reference", "spec"])
+def test_cfg4_long_consensus_many_rounds(mode):
+    """Long-running consensus (the reference re-proposes forever, core/byzantinerandomizedconsensus.py:
+    96-106) on the cfg4 slow-set schedule (D = 8).  Reference protocol: SURVEY cfg4's round cap 64.
+    Its phase leakage (:57-61, :71-78: deliveries of any phase count toward the current one) lets
+    fast replicas end several phases per step, so by round 64 up to 127 phase indices of one origin
+    are in flight and ~7,600 keys of one instance are live at once (oracle-measured): it
+    runs with a key window of 128 on the key-lifetime kernel, which keeps no cells (2^14 instances:
+    its key slots take 115 KB of LDS per wave).  SPEC: round cap 8 with its window of 8 at 2^17.
+    Sampled instances equal the oracle (counters incl. cell-steps, and every replica's first and
+    last decision, values included)."""
+    L = _L()
+    spec = mode == "spec"
+    N, CAP = (1 << 17, 8) if spec else (1 << 14, 64)
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=CAP, step_cap=4000, key_window=8 if spec else 128, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    ids = sorted(random.Random(8).sample(range(N), 5)) + [N - 1]
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        assert eng.last_kernel() == ("step" if spec else "life")
+        st = eng.stats()
+        hist = eng.round_histogram(66)
+        res = {i: eng.instances_result(i, 1)[0] for i in ids}
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    assert st["done"] == N and st["overflow"] == 0       # no BRC_OVERFLOW anywhere in the batch
+    assert hist[0] == 0 and sum(hist) == N
+    if spec:
+        specs = [S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8, coin_seed=0xC017C017)
+                 for g in ids]
+    else:
+        specs = [S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP) for g in ids]
+    for g, (exp, first, last, count) in zip(ids, _oracle_first_last(specs)):
+        for k in KEYS:
+            assert res[g][k] == exp[k], (g, k)
+        for d, r in enumerate(reps[g]):
+            assert (r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) == first[d], (g, d)
+            assert r["last_decide_value"] == last[d] and r["decide_count"] == count[d] >= CAP, (g, d)
+
+
+def test_cfg4_many_rounds_2p20_one_launch():
+    """The bench's many-round leg: the reference protocol to round cap 8 on the cfg4 schedule at the
+    full 2^20 instances in ONE launch.  By round 8 ~1,000 keys of one instance are live at once
+    (oracle-measured), so any cell store would need >= 1,025 x 64 x 4 B per instance = 275 GB: the
+    engine picks the key-lifetime kernel (no cells; key window 32).  Sampled ids equal the oracle."""
+    L = _L()
+    N, CAP = 1 << 20, 8
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=CAP, step_cap=4000, key_window=32, proposals=L.PROPOSALS_PHILOX)
+    ids = sorted(random.Random(64).sample(range(N), 7)) + [N - 1]
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        assert eng.last_kernel() == "life"
+        st = eng.stats()
+        vals, dis = eng.decisions()
+        res = {i: eng.instances_result(i, 1)[0] for i in ids}
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    assert st["done"] == N and st["overflow"] == 0 and dis == 0
+    specs = [S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP) for g in ids]
+    for g, (exp, first, last, count) in zip(ids, _oracle_first_last(specs)):
+        for k in KEYS:
+            assert res[g][k] == exp[k], (g, k)
         for d, r in enumerate(reps[g]):
             assert (r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) == first[d], (g, d)
             assert r["last_decide_value"] == last[d] and r["decide_count"] == count[d] >= CAP, (g, d)
@@ -307,3 +350,54 @@ def test_cfg4_connection_peers_2p20_sampled(model, dmax):
                 assert r["decide_count"] == 0, (g, d)
     if (model, dmax) != ("uniform", 4):
         assert decided > 0
+
+
+def _batch_digest(eng, chunk=1 << 16):
+    """sha256 over every instance's (status, t_stop, msgs, arrivals, cell_steps, deliveries,
+    decided) and every replica's consensus record (round, phase, value_count, decide_count, first
+    decision round / step / value, last value), read in bulk (numpy) chunk by chunk."""
+    import numpy as np
+    h = hashlib.sha256()
+    ikeys = ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps", "deliveries", "decided")
+    for first in range(0, eng.instances, chunk):
+        cnt = min(chunk, eng.instances - first)
+        ia = eng.instances_array(first, cnt)
+        ra = eng.replicas_array(first, cnt)
+        for k in ikeys:
+            h.update(np.ascontiguousarray(ia[k]).tobytes())
+        for k in ra.dtype.names:
+            h.update(np.ascontiguousarray(ra[k]).tobytes())
+    return h.hexdigest()
+
+
+def test_cfg4_2p20_step_kernel_equals_lifetime_kernel():
+    """The bench's whole 2^20 sender-peer cfg4 batch on both kernels (BRC_KERNEL=step: the
+    headline's cell store; BRC_KERNEL=life: the key-lifetime kernel, cells in registers): a digest
+    of every instance's counters (cell-steps included: the roofline's unit) and every replica's
+    consensus record is identical -- not a sample, the whole batch (reference:
+    core/brbroadcast.py:60-119, core/byzantinerandomizedconsensus.py:53-106)."""
+    import os
+    L = _L()
+    N = 1 << 20
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=1, step_cap=4000, key_window=4, proposals=L.PROPOSALS_PHILOX)
+    digests, stats = {}, {}
+    for kernel in ("step", "life"):
+        old = os.environ.get("BRC_KERNEL")
+        os.environ["BRC_KERNEL"] = kernel
+        try:
+            eng = _engine(instance_offset=0, instances=N, **kw)
+        finally:
+            if old is None:
+                os.environ.pop("BRC_KERNEL", None)
+            else:
+                os.environ["BRC_KERNEL"] = old
+        with eng:
+            eng.run()
+            assert eng.last_kernel() == kernel
+            digests[kernel] = _batch_digest(eng)
+            stats[kernel] = eng.stats()
+    assert stats["step"]["done"] == N and stats["step"]["overflow"] == 0
+    for k in ("decided", "msgs_sent", "arrivals", "cell_steps", "deliveries", "decide_rounds_sum"):
+        assert stats["step"][k] == stats["life"][k], k
+    assert digests["step"] == digests["life"]

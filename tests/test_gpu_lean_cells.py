@@ -24,7 +24,7 @@ def _check(got, specs):
     for sp, r in zip(specs, got):
         exp = oracle.run(sp)
         exp["events"] = golden_io.canonical_events(exp["events"])
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert r[k] == exp[k], "%s %s: %r vs oracle %r" % (sp["name"], k, r[k], exp[k])
         for k in ("deliver", "decide", "send"):
             assert r["events"][k] == exp["events"][k], "%s: %s events differ" % (sp["name"], k)
@@ -99,7 +99,7 @@ def test_repeated_resets_rewrite_rows():
                 first = snap
                 for sp, r in zip(specs, res):
                     exp = oracle.run(sp)
-                    for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+                    for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
                         assert r[k] == exp[k], "%s %s" % (sp["name"], k)
             else:
                 assert snap == first, "pass %d differs from the first" % p

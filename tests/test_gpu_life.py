@@ -168,7 +168,7 @@ def test_lifetime_kernel_equals_step_kernel_and_oracle(name):
     for i in random.Random(len(name)).sample(range(count), 6):
         exp = oracle.run(_oracle_spec(kw, offset + i, None if props is None else props[i]))
         r = life["inst"][i]
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert r[k] == exp[k], (name, i, k, r[k], exp[k])
         first = {}
         for t, node, rnd, val in sorted(exp["events"]["decide"]):

@@ -5,7 +5,8 @@ Both ranks share GPU 0 and reduce over gloo (rehearsal backend: the RCCL all-red
 shard of global instance ids through the HIP engine -- the code path the driver's multi-GPU bench
 takes -- and the all-reduced totals must equal ONE rank running every id: Philox draws use global
 ids, so the job's results do not depend on the rank count (weak scaling, no
-data-path exchange).  Both legs (reference protocol and SPEC coin rounds) are checked.
+data-path exchange).  Three legs (reference protocol, SPEC coin rounds, the reference protocol to
+round cap 8) are checked.
 
 torchrun and the single-rank bench are started as child processes before this process touches
 the GPU in this test; nothing replaces a GPU process image.
@@ -46,13 +47,14 @@ def _run(cmd, timeout):
 
 def _legs(d):
     out = {"reference": {k: d[k] for k in KEYS}}
-    out["spec"] = {k: d["spec_leg"][k] for k in KEYS}
+    for leg in ("spec", "many"):
+        out[leg] = {k: d[leg + "_leg"][k] for k in KEYS}
     return out
 
 
 @pytest.mark.gpu
 def test_two_ranks_equal_one_rank_over_the_same_global_ids():
-    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec"]
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many"]
     multi = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(WORLD),
                   "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
                   "--gpus", str(WORLD), "--backend", "gloo", "--instances", str(PER_RANK)] + bench_args, 300)
@@ -60,7 +62,7 @@ def test_two_ranks_equal_one_rank_over_the_same_global_ids():
     assert multi["n_gpus"] == WORLD and single["n_gpus"] == 1
     assert multi["config"]["instances_per_gpu"] * WORLD == single["config"]["instances_per_gpu"]
     m, s = _legs(multi), _legs(single)
-    for leg in ("reference", "spec"):
+    for leg in ("reference", "spec", "many"):
         assert m[leg]["counts"]["instances"] == PER_RANK * WORLD
         assert m[leg]["counts"]["decided"] > 0
         assert m[leg] == s[leg], leg
@@ -72,7 +74,7 @@ def test_rccl_rank_equals_plain_run():
     bound to the GPU (`device_id`): the statistics go through the device all-reduce of
     `shard.reduce_stats` / `max_over_ranks` -- the 8-GPU path's collective, run on the one leased
     GPU -- and must equal the plain single-process run over the same global ids."""
-    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec",
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many",
                   "--instances", str(PER_RANK * WORLD)]
     rccl = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
@@ -81,6 +83,6 @@ def test_rccl_rank_equals_plain_run():
     assert rccl["collective"] == "nccl all-reduce of the statistics"
     assert single["collective"] is None
     r, s = _legs(rccl), _legs(single)
-    for leg in ("reference", "spec"):
+    for leg in ("reference", "spec", "many"):
         assert r[leg]["counts"]["decided"] > 0
         assert r[leg] == s[leg], leg

@@ -26,6 +26,8 @@ def test_engine_matches_reference_fixtures(runner, group):
     got = runner.run_specs([c["spec"] for c in cases])
     for i, (c, r) in enumerate(zip(cases, got)):
         golden_io.assert_matches(c["result"], r, "%s[%d]" % (group, i))
+        # the roofline's unit: cell-steps equal the oracle's on the reference-pinned schedule
+        assert r["cell_steps"] == golden_io.cell_steps(group, i), (group, i, r["cell_steps"])
 
 
 def _compare_with_oracle(runner, specs):
@@ -33,7 +35,7 @@ def _compare_with_oracle(runner, specs):
     for sp, r in zip(specs, got):
         exp = oracle.run(sp)
         exp["events"] = golden_io.canonical_events(exp["events"])
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert r[k] == exp[k], "%s %s: %r vs oracle %r" % (sp["name"], k, r[k], exp[k])
         for k in ("deliver", "decide", "send"):
             assert r["events"][k] == exp["events"][k], "%s: %s events differ" % (sp["name"], k)

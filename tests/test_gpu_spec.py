@@ -23,7 +23,7 @@ def _compare(runner, specs):
     for sp, r in zip(specs, got):
         exp = oracle.run(sp)
         exp["events"] = golden_io.canonical_events(exp["events"])
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert r[k] == exp[k], "%s %s: %r vs oracle %r" % (sp["name"], k, r[k], exp[k])
         for k in ("deliver", "decide", "send"):
             assert r["events"][k] == exp["events"][k], "%s: %s events differ" % (sp["name"], k)

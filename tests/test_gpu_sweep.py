@@ -78,7 +78,7 @@ def test_sweep_batch_matches_oracle_samples(f):
         res = eng.instances_result()
         reps = {c["g"]: eng.replicas(c["g"], 1)[0] for c in cases}
     for c in cases:
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert res[c["g"]][k] == c[k], (f, c["g"], k)
         for d, (rep, exp) in enumerate(zip(reps[c["g"]], c["first_decide"])):
             assert exp is not None, (c["g"], d)

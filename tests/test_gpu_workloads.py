@@ -39,7 +39,7 @@ def _compare(runner, specs):
     for sp, r in zip(specs, got):
         exp = oracle.run(sp)
         exp["events"] = golden_io.canonical_events(exp["events"])
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert r[k] == exp[k], "%s %s: %r vs oracle %r" % (sp["name"], k, r[k], exp[k])
         for k in ("deliver", "decide", "send"):
             assert r["events"][k] == exp["events"][k], "%s: %s events differ" % (sp["name"], k)
@@ -100,7 +100,7 @@ def test_equivocation_pattern_wide_matches_oracle():
     for g in (0, 77, N - 1):
         exp = oracle.run(S.cons_spec(n, f, 0x5EED0006, 1, 4, g, round_cap=1, byzantine=byz, nv=2,
                                      extra=S.equivocation_actions(n, byz)))
-        for k in ("status", "t_stop", "msgs_sent", "arrivals"):
+        for k in ("status", "t_stop", "msgs_sent", "arrivals", "cell_steps"):
             assert res[g][k] == exp[k], (g, k)
 
 

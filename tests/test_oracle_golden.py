@@ -14,6 +14,7 @@ def test_oracle_matches_reference(group, idx):
     case = GROUPS[group][idx]
     got = oracle.run(case["spec"])
     golden_io.assert_matches(case["result"], got, "%s[%d]" % (group, idx))
+    assert got["cell_steps"] == golden_io.cell_steps(group, idx), (group, idx)
 
 
 @pytest.mark.slow
@@ -24,6 +25,7 @@ def test_oracle_matches_reference_large(group):
     case = GROUPS[group][0]
     got = oracle.run(case["spec"])
     golden_io.assert_matches(case["result"], got, group)
+    assert got["cell_steps"] == golden_io.cell_steps(group, 0), group
 
 
 RAW = [(g, i) for g, cases in GROUPS.items() for i, c in enumerate(cases) if "raw_order" in c["result"]]

@@ -6,7 +6,7 @@ TAGS=$1; ROUNDS=$2; ONLY=$3
 mkdir -p gpurun_out/abcfg
 for r in $(seq 1 $ROUNDS); do
   for t in $TAGS; do
-    if [ "$t" = head ]; then lib=""; else lib=exp/$t/libbrc_hip.so; fi
+    if [ "$t" = head ]; then lib=""; else lib=ab/$t/libbrc_hip.so; fi
     BRC_LIB=$lib timeout -k 10 300 python3 configs.py --only $ONLY --steps 2 --warmup 1 > gpurun_out/abcfg/$t.$r.jsonl 2> gpurun_out/abcfg/$t.$r.err || { echo "FAIL $t round $r"; tail -5 gpurun_out/abcfg/$t.$r.err; exit 1; }
     python3 -c "
 import json,sys

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Build an A/B variant of libbrc_hip.so with extra compile flags (dev tool, not the product build).
 
-    python tools/variant.py <tag> [-DFLAG=V ...]   ->  exp/<tag>/libbrc_hip.so
+    python tools/variant.py <tag> [-DFLAG=V ...]   ->  ab/<tag>/libbrc_hip.so
 
-exp/ is git-ignored but travels to the GPU box with gpurun; select a variant there with
-BRC_LIB=exp/<tag>/libbrc_hip.so (byzantinerandomizedconsensus_amd/_lib.py).
+ab/ is git-ignored but travels to the GPU box with gpurun; select a variant there with
+BRC_LIB=ab/<tag>/libbrc_hip.so (byzantinerandomizedconsensus_amd/_lib.py).
 """
 import os
 import subprocess
@@ -17,7 +17,7 @@ import __graft_entry__ as G  # noqa: E402
 
 def main():
     tag, flags = sys.argv[1], sys.argv[2:]
-    out = os.path.join(ROOT, "exp", tag)
+    out = os.path.join(ROOT, "ab", tag)
     os.makedirs(out, exist_ok=True)
     procs, objs = [], []
     for unit in G.HIP_UNITS:

@@ -170,6 +170,7 @@ struct Engine {
     uint64_t* dring = nullptr;                   // per-link lifetime kernel: delivery bitmap ring (brc_life.h)
     uint64_t* xsend = nullptr; uint32_t* xsn = nullptr;   // extra-SEND records (non-lean step kernels)
     bool life_pl = false;                        // lifetime kernel in its per-link delay form
+    uint32_t life_rw = LIFE_RW;                  // ... its delivery-ring rows (LIFE_RW16 for delays above 8)
     uint32_t nval = 4;                           // consensus value ids the step kernel keeps (value_ids)
     bool values_wide = false;                    // a loaded proposal uses a value id >= 4 (no lifetime kernel)
     Params* dparams = nullptr;                   // device copy of the launch parameters
@@ -446,9 +447,10 @@ int brc_create(const brc_config* cfg, void** out) {
         const bool force_step = kv && strcmp(kv, "step") == 0, force_life = kv && strcmp(kv, "life") == 0;
         e->life_lds = lds_bytes_life(e->NK, e->nkw, spec, c.key_window, c.variants);
         e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
+        e->life_rw = (e->life_pl && c.delay_max > 8) ? LIFE_RW16 : LIFE_RW;
         const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
                               c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
-                              c.delay_max <= 8 && e->life_lds <= 160 * 1024 &&
+                              c.delay_max <= (e->life_pl ? 16u : 8u) && e->life_lds <= 160 * 1024 &&
                               // per-link form: its HBM delivery ring is [RW][NK] bits per instance
                               !(e->life_pl && c.key_window * c.variants > 32);
         bool big = e->compact && c.key_window * c.variants > 32;          // the lean kernels take <= 32
@@ -463,7 +465,7 @@ int brc_create(const brc_config* cfg, void** out) {
         if (big && !e->life_cfg) {
             g_create_err = c.key_window * c.variants > 32
                 ? "key windows above 32 at n in 33..64 with sender peers run on the key-lifetime kernel only "
-                  "(consensus, Philox / loaded proposals, delay_max <= 8, constant / slow-set delays, no event log)"
+                  "(consensus, Philox / loaded proposals, delay_max <= 8, constant or slow-set delays, no event log)"
                 : "the step kernel's cells do not fit in free device memory and the key-lifetime kernel cannot run "
                   "this configuration";
             delete e;
@@ -498,7 +500,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->inj_cnt, (size_t)e->nitems * 4}, {(void**)&e->byz, c.instances * e->bw * 8}, {(void**)&e->gcount, 64},
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec && e->step_ok) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
-        {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8 : 8},
+        {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * e->life_rw * e->nkw * 64 * 8 : 8},
         // extra-SEND records: the non-lean narrow kernels only (the lean and wide kernels refuse extra SENDs)
         {(void**)&e->xsend, (e->compact || e->wide) ? 8 : (size_t)e->nitems * XSEND_MAX * 24},
         {(void**)&e->xsn, (e->compact || e->wide) ? 8 : (size_t)e->nitems * 4},
@@ -518,7 +520,7 @@ int brc_create(const brc_config* cfg, void** out) {
     if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);   // keys = 1: 8 B
     // the lifetime kernel leaves its bitmap ring zero at exit
     if (e->life_cfg && e->life_pl &&
-        hipMemsetAsync(e->dring, 0, (size_t)e->nitems * LIFE_RW * e->nkw * 64 * 8, e->stream) != hipSuccess)
+        hipMemsetAsync(e->dring, 0, (size_t)e->nitems * e->life_rw * e->nkw * 64 * 8, e->stream) != hipSuccess)
         return fail(BRC_E_HIP);
     {
         std::vector<uint64_t> bm((size_t)c.instances * e->bw);
@@ -805,7 +807,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     e->fresh = false;
     e->last_life = life;
     if (life) {
-        rc = launch_life(kmode, e->life_pl, (uint32_t)e->nitems, e->life_lds, e->stream, e->dparams);
+        rc = launch_life(kmode, e->life_pl, e->life_rw == LIFE_RW16, c.key_window >= 64, (uint32_t)e->nitems,
+                         e->life_lds, e->stream, e->dparams);
         e->life_done = true;
     } else {
         rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)

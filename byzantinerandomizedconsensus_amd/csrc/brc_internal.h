@@ -100,7 +100,7 @@ struct Params {
     const uint64_t* byz; const int8_t* prop;
     brc_event* events; unsigned long long* event_count;
     uint64_t* dbits;              // lean SPEC: per-wave delivery bitmaps [item][nkw][64] (brc_step.h DBG)
-    uint64_t* dring;              // per-link key-lifetime kernel: delivery bitmap ring [item][LIFE_RW][nkw][64] (brc_life.h)
+    uint64_t* dring;              // per-link key-lifetime kernel: delivery bitmap ring [item][LIFE_RW or LIFE_RW16][nkw][64] (brc_life.h)
     uint64_t* xsend;              // non-lean step kernels: extra-SEND records [item][XSEND_MAX][3] (brc_step.h)
     uint32_t* xsn;                // ... records in use per item
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
@@ -208,8 +208,12 @@ __host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, uint32_t nkw, bo
     return 4 * NK + ((2 * NK + 7) & ~7u) + 2 * LIFE_RW * nkw * 8 + LIFE_RW * 16 + 8 * cons_words(spec, 8, Q, nv) + 256;
 }
 // Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
-// (perlink: uniform / geometric delays, delivery bitmaps in P.dring)
-int launch_life(int mode, bool perlink, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+// (perlink: uniform / geometric delays, delivery bitmaps in P.dring; dm16: delays up to 16, whose
+// keys live up to 64 steps: P.dring has LIFE_RW16 rows)
+constexpr uint32_t LIFE_RW16 = 64;
+// qbig: key windows of 64 / 128 (two-class form, not SPEC)
+int launch_life(int mode, bool perlink, bool dm16, bool qbig, uint32_t blocks, uint32_t lds, hipStream_t s,
+                const Params* P);
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).
 // Return 0 on success, BRC_E_INVALID when no instantiation matches (dm), BRC_E_HIP on a launch error.

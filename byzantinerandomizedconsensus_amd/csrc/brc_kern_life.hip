@@ -4,16 +4,26 @@
 #include "brc_life.h"
 
 namespace brc {
-template <bool PL>
+template <bool PL, int DLX>
 static int launch_life_pl(int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    if (mode == BRC_MODE_SPEC) return launch_life_one<BRC_MODE_SPEC, PL>(blocks, lds, s, P);
-    if (mode == BRC_MODE_BEB) return launch_life_one<BRC_MODE_BEB, PL>(blocks, lds, s, P);
-    if (mode == BRC_MODE_REFERENCE) return launch_life_one<BRC_MODE_REFERENCE, PL>(blocks, lds, s, P);
-    if (mode == KMODE_CONN) return launch_life_one<KMODE_CONN, PL>(blocks, lds, s, P);
+    if (mode == BRC_MODE_SPEC) return launch_life_one<BRC_MODE_SPEC, PL, DLX>(blocks, lds, s, P);
+    if (mode == BRC_MODE_BEB) return launch_life_one<BRC_MODE_BEB, PL, DLX>(blocks, lds, s, P);
+    if (mode == BRC_MODE_REFERENCE) return launch_life_one<BRC_MODE_REFERENCE, PL, DLX>(blocks, lds, s, P);
+    if (mode == KMODE_CONN) return launch_life_one<KMODE_CONN, PL, DLX>(blocks, lds, s, P);
     return BRC_E_INVALID;
 }
-// perlink: uniform / geometric delays (per-receiver delay masks, HBM delivery bitmaps)
-int launch_life(int mode, bool perlink, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    return perlink ? launch_life_pl<true>(mode, blocks, lds, s, P) : launch_life_pl<false>(mode, blocks, lds, s, P);
+// perlink: uniform / geometric delays (per-receiver delay masks, HBM delivery bitmaps); dm16: delays up
+// to 16 (the per-link form's 64-row ring); qbig: key windows of 64 / 128 (two-class form, not SPEC)
+int launch_life(int mode, bool perlink, bool dm16, bool qbig, uint32_t blocks, uint32_t lds, hipStream_t s,
+                const Params* P) {
+    if (qbig) {
+        if (perlink || mode == BRC_MODE_SPEC) return BRC_E_INVALID;
+        if (mode == BRC_MODE_BEB) return launch_life_one<BRC_MODE_BEB, false, 8, true>(blocks, lds, s, P);
+        if (mode == BRC_MODE_REFERENCE) return launch_life_one<BRC_MODE_REFERENCE, false, 8, true>(blocks, lds, s, P);
+        if (mode == KMODE_CONN) return launch_life_one<KMODE_CONN, false, 8, true>(blocks, lds, s, P);
+        return BRC_E_INVALID;
+    }
+    if (perlink && dm16) return launch_life_pl<true, 16>(mode, blocks, lds, s, P);
+    return perlink ? launch_life_pl<true, 8>(mode, blocks, lds, s, P) : launch_life_pl<false, 8>(mode, blocks, lds, s, P);
 }
 }  // namespace brc

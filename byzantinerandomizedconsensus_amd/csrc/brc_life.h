@@ -59,11 +59,18 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 #ifndef BRC_LIFE_PL_CONN_WAVES
 #define BRC_LIFE_PL_CONN_WAVES 6   // per-link form, connection peers: waves per SIMD (A/B: 5 284.4, 6 273.2, 7 277.5 ms)
 #endif
-template <int MODE, bool PL>
+// DLX: per-link form's largest delay (8, or 16: cfg5's geometric cap), whose keys live up to 4 DLX steps:
+// RW = 64 ring rows then (step statistics in 64 lanes, delivery bitmaps in a 64-row HBM ring).
+// QBIG: key windows of 64 / 128 (the reference protocol's many-round runs), two-class form only.  Both
+// are instantiations of their own, so the default ones keep their registers.
+template <int MODE, bool PL, int DLX = 8, bool QBIG = false>
 __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAVES : 6) : 8) void brc_life(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
-    constexpr uint32_t RW = LIFE_RW;
+    static_assert(DLX == 8 || (PL && DLX == 16), "delays up to 16: per-link form");
+    static_assert(!(QBIG && (PL || MODE == BRC_MODE_SPEC)), "key windows above 32: two-class form, not SPEC");
+    constexpr uint32_t RW = (PL && DLX > 8) ? 64u : LIFE_RW;     // ring rows (> the longest key lifetime)
+    constexpr uint64_t RWM = RW == 64 ? ~0ull : ((1ull << RW) - 1ull);
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const uint32_t lane = threadIdx.x;
     const uint64_t item = blockIdx.x;
@@ -76,10 +83,11 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // ---- LDS carve (lds_bytes_life)
     uint32_t* s_meta = (uint32_t*)smem;
     uint16_t* s_snap = (uint16_t*)(s_meta + NK);
+    // two-class delivery rings (LIFE_RW rows; the per-link form keeps its deliveries in HBM, P.dring)
     uint64_t* s_dkA = (uint64_t*)((char*)smem + 4 * NK + ((2 * NK + 7) & ~7u));
-    uint64_t* s_dkB = s_dkA + RW * nkw;
-    uint64_t* s_ring = s_dkB + RW * nkw;          // [row][2]: arrivals | msgs << 32, cells | deliveries << 32
-    uint64_t* s_hm = s_ring + 2 * RW;             // REFERENCE / BEB: hosts per value [4][64]
+    uint64_t* s_dkB = s_dkA + LIFE_RW * nkw;
+    uint64_t* s_ring = s_dkB + LIFE_RW * nkw;     // [row][2]: arrivals | msgs << 32, cells | deliveries << 32
+    uint64_t* s_hm = s_ring + 2 * LIFE_RW;        // REFERENCE / BEB: hosts per value [4][64]
     uint64_t* s_seen = s_hm;                      // SPEC, NV > 1: [Q][64]
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));   // SPEC: [Q][64]
     // CONN: READY copies landing at relative step r of the key being simulated, per receiver class:
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 
     // ---- PL: per-link delay masks (brc_step.h link-delay masks, NPAD = 64): L[i] = senders j whose
     // link j -> d has delay i+1; OV[i] (wave-uniform) = senders with a delay-(i+1) link to an honest receiver
-    constexpr int DL = PL ? 8 : 1;
+    constexpr int DL = PL ? DLX : 1;
     uint64_t L[DL], OV[DL];
 #pragma unroll
     for (int i = 0; i < DL; ++i) L[i] = OV[i] = 0;
@@ -162,7 +170,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) { s_meta[i] = 0; s_snap[i] = 0; }
-    for (uint32_t i = lane; i < 2 * RW * nkw; i += 64) s_dkA[i] = 0;
+    for (uint32_t i = lane; i < 2 * LIFE_RW * nkw; i += 64) s_dkA[i] = 0;
     if constexpr (SPEC) {
         for (uint32_t q = 0; q < Q; ++q) {
             if (seen_on) s_seen[q * 64 + lane] = 0;
@@ -185,15 +193,16 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         return ((uint64_t)uni32(rl((uint32_t)(acc >> 32), l)) << 32) | uni32(rl((uint32_t)acc, l));
     };
     uint32_t st_smax = 0;
-    uint32_t rows = 0;                             // ring rows holding arrivals at honest receivers
+    using RowT = typename std::conditional<RW == 64, uint64_t, uint32_t>::type;
+    RowT rows = 0;                                 // ring rows holding arrivals at honest receivers
 
     // ---- consensus state (core/byzantinerandomizedconsensus.py:25-29)
     const bool cons_lane = honest;                 // consensus protocol (host-checked)
     uint32_t round = 0, phase = 0, nvals = 0, order = 0, vcount = 0;
     uint32_t dcount = 0, frnd = 0, ft = 0, fval = 0, lval = 0;
-    // this lane's keys created this step: phase indices clr_s .. clr_s + clr_n - 1 (a replica's SENDs of
-    // one step have consecutive indices: each phase end advances the index by one)
-    uint32_t clr_s = 0, clr_n = 0;
+    // this lane's keys created this step: bit s mod Q (Q <= 32), or (QBIG) phase indices clr_s .. clr_s +
+    // clr_n - 1 (a replica's SENDs of one step have consecutive indices: each phase end advances it by one)
+    uint32_t clr = 0, clr_s = 0, clr_n = 0;
     uint32_t msg_now = 0;                          // SEND messages sent this step (per lane, counted at once)
 
     // honest origin d broadcasts SEND for its key (d, s) with value v (core/byzantinerandomizedconsensus.py:48-50,
@@ -203,8 +212,12 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t m = s_meta[k];
         if ((lm_s1(m) != 0 && t < lm_tend(m)) || s >= 0x3FFEu) { ovf = true; return; }
         s_meta[k] = ((t + 1u) << 16) | ((v & 3u) << 14) | (s + 1u);   // busy until simulated
-        if (clr_n == 0) clr_s = s;
-        ++clr_n;
+        if constexpr (QBIG) {
+            if (clr_n == 0) clr_s = s;
+            ++clr_n;
+        } else {
+            clr |= 1u << (s & Qm);
+        }
         msg_now += n;
         st_smax = max(st_smax, s);
     };
@@ -294,17 +307,18 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t t0 = t;
         // SEND arrivals: fast receivers at 1 if the origin is fast, everyone else at Dd
         uint32_t sdl = (oF && laneF) ? 1u : Dd;
-        uint64_t pendS = 0, pendE = 0, pendR = 0;     // relative steps with SEND / ECHO / READY arrivals
+        // relative steps with SEND / ECHO / READY arrivals: bit i <=> step i + 1 (steps 1 .. RW <= 64)
+        uint64_t pendS = 0, pendE = 0, pendR = 0;
         if constexpr (PL) {
             sdl = 0;
 #pragma unroll
             for (int i = 0; i < DL; ++i) {
                 if ((L[i] >> o) & 1ull) sdl = (uint32_t)i + 1u;
-                if ((OV[i] >> o) & 1ull) pendS |= 2ull << i;
+                if ((OV[i] >> o) & 1ull) pendS |= 1ull << i;
             }
         } else {
-            if (oF && HF) pendS |= 1ull << 1;
-            if (HS || (!oF && HF)) pendS |= 1ull << Dd;
+            if (oF && HF) pendS |= 1ull;
+            if (HS || (!oF && HF)) pendS |= 1ull << (Dd - 1u);
         }
         uint32_t fl = 0, ec = 0, rc = 0, rE = LIFE_NEVER, rR = LIFE_NEVER;
         Ring16 ringR = {0ull, 0ull};                  // PL connection peers: READY copies per step
@@ -313,8 +327,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t kw = k >> 6;
         const uint64_t kbit = 1ull << (k & 63);
         for (uint64_t pend = pendS; pend; pend = pendS | pendE | pendR) {
-            const uint32_t r = (uint32_t)__builtin_ctzll(pend);
-            const uint64_t rb = 1ull << r;
+            const uint32_t r = (uint32_t)__builtin_ctzll(pend) + 1u;
+            const uint64_t rb = 1ull << (r - 1u);
             const bool hS = (pendS & rb) != 0, hE = (pendE & rb) != 0, hR = (pendR & rb) != 0;
             pendS &= ~rb; pendE &= ~rb; pendR &= ~rb;
             if (r > RW) { ovf = true; break; }        // two-class: cannot happen for Dd <= 8 (lifetime <= 4 Dd)
@@ -488,21 +502,26 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 // a message sent now lands after every delay i+1 some link of its sender has to an honest
                 // receiver: the senders' delay sets OR-ed over the wave (one DPP reduction, VALU)
                 if (eb | rbm) {
-                    uint32_t x = (es ? myout : 0u) | ((rs ? myout : 0u) << 8);
+                    uint32_t x = (es ? myout : 0u) | ((rs ? myout : 0u) << DL);
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);
                     x = uni32(rl(x, 0) | rl(x, 16) | rl(x, 32) | rl(x, 48));
-                    pendE |= (uint64_t)(x & 0xFFu) << (r + 1);
-                    pendR |= (uint64_t)(x >> 8) << (r + 1);
+                    // arrivals at r + i + 1 for every delay bit i: bit r + i (past the ring: overflow, never lost)
+                    constexpr uint32_t DM1 = (1u << DL) - 1u;
+                    if (r + hibit(x & DM1) > RW || r + hibit(x >> DL) > RW) ovf = true;
+                    pendE |= (uint64_t)(x & DM1) << r;
+                    pendR |= (uint64_t)(x >> DL) << r;
                 }
             } else if (eb) {
+                if (r + Dd > RW) ovf = true;
                 if ((eb & Fm) && HF) pendE |= rb << 1;
                 if (HS || ((eb & Sm) && HF)) pendE |= rb << Dd;
             }
             if (!PL && rbm) {
                 const bool at1 = cF && HF, atD = HS || (cS && HF);
+                if (r + Dd > RW) ovf = true;
                 if (at1) pendR |= rb << 1;
                 if (atD) pendR |= rb << Dd;
                 if constexpr (CONN) {
@@ -515,24 +534,36 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 rg_arr += mine ? arr : 0u; rg_msg += mine ? msgs : 0u;
                 rg_cell += mine ? cells : 0u; rg_del += mine ? dels : 0u;
             }
-            rows |= 1u << row;
+            rows |= (RowT)1 << row;
             last = ts;
         }
         if (lane == 0) s_meta[k] = (s_meta[k] & 0xFFFFu) | (last << 16);
     };
     // the keys created this step (every lane's clr_s .. clr_s + clr_n - 1), each simulated once
     auto simulate_new = [&]() {
-        for (uint64_t b = __ballot(clr_n != 0); b; b &= b - 1) {
-            const int L = __ffsll((unsigned long long)b) - 1;
-            const uint32_t s0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_s, L));
-            const uint32_t cn = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_n, L));
-            for (uint32_t i = 0; i < cn; ++i) {
-                const uint32_t k = ((uint32_t)L * NV) * Q + ((s0 + i) & Qm);
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                simulate(k);
+        if constexpr (QBIG) {
+            for (uint64_t b = __ballot(clr_n != 0); b; b &= b - 1) {
+                const int L = __ffsll((unsigned long long)b) - 1;
+                const uint32_t s0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_s, L));
+                const uint32_t cn = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr_n, L));
+                for (uint32_t i = 0; i < cn; ++i) {
+                    const uint32_t k = ((uint32_t)L * NV) * Q + ((s0 + i) & Qm);
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    simulate(k);
+                }
             }
+            clr_n = 0;
+        } else {
+            for (uint64_t b = __ballot(clr != 0); b; b &= b - 1) {
+                const int L = __ffsll((unsigned long long)b) - 1;
+                for (uint32_t cm = uni32((uint32_t)__builtin_amdgcn_readlane((int)clr, L)); cm; cm &= cm - 1) {
+                    const uint32_t k = ((uint32_t)L * NV) * Q + (uint32_t)__ffs(cm) - 1u;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    simulate(k);
+                }
+            }
+            clr = 0;
         }
-        clr_n = 0;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     };
 
@@ -554,9 +585,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     while (status == BRC_RUNNING) {
         // next step with arrivals at an honest receiver
         const uint32_t rot = (t + 1) & (RW - 1);
-        const uint32_t rr = rot ? ((rows >> rot) | (rows << (RW - rot))) : rows;
+        const RowT rr = (RowT)((rot ? ((rows >> rot) | (rows << (RW - rot))) : rows) & RWM);
         if (!rr) { status = BRC_QUIESCENT; break; }
-        const uint32_t next = t + 1 + (uint32_t)__ffs(rr) - 1u;
+        const uint32_t next = t + 1 + (uint32_t)__builtin_ctzll(rr);
         if (next > P.step_cap) { status = BRC_STEPCAP; break; }
         t = uni32(next);
         const uint32_t row = t & (RW - 1);
@@ -584,7 +615,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             }
             return bits;
         };
-        if (Q >= 64) {
+        if constexpr (QBIG) {
             // key windows of 64 / 128 (the reference protocol's many-round runs): a key prefix
             // (origin, variant) spans Q / 64 whole words; its deliveries of one step (one origin) go one
             // at a time, smallest phase index first -- the canonical (kp, s) order
@@ -693,7 +724,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         // the step is consumed: its ring row is free for step t + RW
         for (uint32_t i = lane; i < 2 * nkw; i += 64) (i < nkw ? s_dkA : s_dkB)[row * nkw + (i % nkw)] = 0;
         if (lane == row) { rg_arr = 0; rg_msg = 0; rg_cell = 0; rg_del = 0; }
-        rows &= ~(1u << row);
+        rows &= ~((RowT)1 << row);
         // ================= per-instance stop conditions (brc_step.h)
         const uint64_t b_und = __ballot(honest && dcount < P.round_cap);
         if (__ballot(ovf)) status = BRC_OVERFLOW;
@@ -704,8 +735,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     if (__ballot(ovf) && status != BRC_OVERFLOW) status = BRC_OVERFLOW;
     if constexpr (PL) {
         // rows of steps the instance did not reach: leave the bitmap ring zero for the next launch
-        for (uint32_t rm = rows; rm; rm &= rm - 1) {
-            const uint32_t row = (uint32_t)__ffs(rm) - 1u;
+        for (uint64_t rm = rows; rm; rm &= rm - 1) {
+            const uint32_t row = (uint32_t)__builtin_ctzll(rm);
             for (uint32_t w = 0; w < nkw; ++w)
                 __hip_atomic_store(dring + (row * nkw + w) * 64, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -742,9 +773,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     }
 }
 
-template <int MODE, bool PL>
+template <int MODE, bool PL, int DLX = 8, bool QBIG = false>
 int launch_life_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_life<MODE, PL>;
+    auto kern = brc_life<MODE, PL, DLX, QBIG>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;

@@ -1678,7 +1678,7 @@ void brc_step(const Params* __restrict__ pp) {
                 });
                 // the refill entries p + LC .. p + 2 LC - 1 in 8-B reads (p % 4 == 0 and s_klist
                 // is 8-B aligned), so a refill never waits on an LDS round trip of its own
-                static_assert(LC == 4 || LC == 8, "four or eight key-list entries per refill");
+                static_assert(LC == 4 || LC == 8 || LC == 16, "four, eight or sixteen key-list entries per refill");
                 uint64_t knext[LC / 2];           // entries 2i | 2i + 1 << 32
                 Unrolled<LC / 4>::run([&](auto qi) {
                     constexpr int q = decltype(qi)::value;

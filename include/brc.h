@@ -90,10 +90,12 @@ typedef struct {
     uint32_t delay_const;     /* BRC_DELAY_CONST value */
     uint32_t round_cap;       /* consensus: instance DONE when every honest replica decided this many times */
     uint32_t step_cap;        /* last simulated step (<= 60000) */
-    uint32_t key_window;      /* Q: live phase indices per origin (2, 4, 8; 16 or 32 with n <= 64 and the
+    uint32_t key_window;      /* Q: live phase indices per origin (2, 4, 8; 16 .. 128 with n <= 64 and the
                                  reference / best-effort protocols, whose phase leakage keeps up to ~17
-                                 phases of one origin in flight by round 8 under slow-set D = 8) */
-    uint32_t variants;        /* NV: key variants per origin (1, 2 or 4; Q*NV <= 8, <= 32 where Q may be) */
+                                 phases of one origin in flight by round 8 and 127 by round 64 under
+                                 slow-set D = 8; above 32 at n in 33..64 with sender peers: the
+                                 key-lifetime kernel only) */
+    uint32_t variants;        /* NV: key variants per origin (1, 2 or 4; Q*NV <= 8, <= 128 where Q may be) */
     uint32_t proposals;       /* BRC_PROPOSALS_* (consensus) */
     uint32_t byz_pattern;     /* BRC_BYZ_* applied to every instance */
     uint32_t event_capacity;  /* 0: no event log */
@@ -196,14 +198,15 @@ int brc_read_events_range(void* engine, size_t first, brc_event* out, size_t cap
 int brc_last_kernel_ms(void* engine, float* ms);
 /* Which kernel the last brc_run launched.  BRC_KERNEL_LIFE (the key-lifetime kernel) runs a fresh
  * engine (after brc_create / brc_reset) to completion in one launch when the configuration allows:
- * n in 33..64, consensus with Philox or loaded proposals, delay_max <= 8 under any delay model
- * (constant / slow-set: its two-class form; uniform / geometric: its per-link form, which keeps a
- * 64 KB-per-instance delivery-bitmap ring in HBM at NK = 256), no event log, no byz_pattern, no
- * injections, max_steps == 0.  By default it runs
- * connection-identity peers (BRC_PEER_CONNECTION); the environment variable BRC_KERNEL (read by
- * brc_create) = life uses it for sender peers too, = step never.  Its results equal the step
- * kernel's; its instances end final, so a later injection that would re-open a QUIESCENT instance
- * is BRC_E_STATE until brc_reset. */
+ * n in 33..64, consensus with Philox or loaded proposals, constant / slow-set delays with
+ * delay_max <= 8 (its two-class form) or uniform / geometric delays with delay_max <= 16 (its
+ * per-link form, which keeps a delivery-bitmap ring in HBM: 64 KB per instance at NK = 256, 128 KB
+ * for delays above 8), no event log, no byz_pattern, no injections, max_steps == 0.  By default it
+ * runs connection-identity peers (BRC_PEER_CONNECTION), and sender peers whose step-kernel cells
+ * would not fit in free device memory or whose key window is above 32; the environment variable
+ * BRC_KERNEL (read by brc_create) = life uses it for every eligible engine, = step never.  Its
+ * results equal the step kernel's; its instances end final, so a later injection that would
+ * re-open a QUIESCENT instance is BRC_E_STATE until brc_reset. */
 enum { BRC_KERNEL_STEP = 0, BRC_KERNEL_LIFE = 1 };
 int brc_last_kernel(void* engine, uint32_t* kind);
 int brc_device_count(int* count);

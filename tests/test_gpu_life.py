@@ -84,6 +84,13 @@ def _workloads():
                                   round_cap=3, key_window=8, peer_mode=L.PEER_CONNECTION),
         "conn-geo64": dict(base, n=64, f=21, seed=0x6E0064, delay_model=L.DELAY_GEOMETRIC, delay_max=8, round_cap=1,
                            key_window=4, peer_mode=L.PEER_CONNECTION),
+        # delays up to 16 (cfg5's geometric cap): the per-link form's 64-row ring
+        "conn-geo64-d16": dict(base, n=64, f=21, seed=0x6E1664, delay_model=L.DELAY_GEOMETRIC, delay_max=16,
+                               round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION),
+        "conn-unif50-d12-r2": dict(base, n=50, f=16, seed=0xC0D12, delay_model=L.DELAY_UNIFORM, delay_max=12,
+                                   round_cap=2, key_window=8, peer_mode=L.PEER_CONNECTION),
+        "ref-geo64-d16-cap40": dict(base, n=64, f=21, seed=0x5EED1664, delay_model=L.DELAY_GEOMETRIC, delay_max=16,
+                                    round_cap=0, key_window=16, step_cap=40),
         "conn-unif45-byz": dict(base, n=45, f=14, seed=0xC0AD45, delay_model=L.DELAY_UNIFORM, delay_max=3, round_cap=2,
                                 key_window=8, byzantine=[1, 30], peer_mode=L.PEER_CONNECTION),
         "ref-unif64-d2-r3": dict(base, n=64, f=21, seed=0x5EED0044, delay_model=L.DELAY_UNIFORM, delay_max=2,
@@ -184,7 +191,7 @@ def test_lifetime_kernel_equals_step_kernel_and_oracle(name):
 
 def test_kernel_choice():
     """Default choice: connection peers run on the lifetime kernel, sender peers on the step kernel
-    (faster there); event logs, injections, stepped runs and delays past 8 stay on the step kernel;
+    (faster there); event logs, injections, stepped runs and two-class delays past 8 stay on the step kernel;
     a lifetime-run instance cannot be re-opened by an injection."""
     from byzantinerandomizedconsensus_amd.engine import Engine
     L = _L()
@@ -208,7 +215,10 @@ def test_kernel_choice():
         assert eng.last_kernel() == "life"                # per-link form
     with Engine(instances=4, **dict(kw, delay_model=L.DELAY_GEOMETRIC, delay_max=16)) as eng:
         eng.run()
-        assert eng.last_kernel() == "step"                # D > 8
+        assert eng.last_kernel() == "life"                # per-link form, delays up to 16 (64-row ring)
+    with Engine(instances=4, **dict(kw, delay_max=12)) as eng:
+        eng.run()
+        assert eng.last_kernel() == "step"                # two-class form: D <= 8
     with Engine(instances=4, **kw) as eng:
         eng.inject([dict(t=0, kind=L.INJ_PROPOSE, instance=0, node=0, value=1)])
         eng.run()

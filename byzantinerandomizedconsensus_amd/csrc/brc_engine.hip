@@ -292,7 +292,7 @@ static int clear_state(Engine* e, bool full) {
         HIPCHK(e, hipGetLastError());
     }
     if (e->step_ok)
-        HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8, e->stream));
+        HIPCHK(e, hipMemsetAsync(e->act, 0, (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact, e->ipw) * 8, e->stream));
     HIPCHK(e, hipMemsetAsync(e->actany, 0, (size_t)e->nitems * 4, e->stream));
     HIPCHK(e, hipMemsetAsync(e->items, 0, (size_t)e->nitems * sizeof(ItemState), e->stream));
     HIPCHK(e, hipMemsetAsync(e->inst, 0, (size_t)e->cfg.instances * sizeof(InstState), e->stream));
@@ -445,8 +445,8 @@ int brc_create(const brc_config* cfg, void** out) {
     {
         const char* kv = getenv("BRC_KERNEL");
         const bool force_step = kv && strcmp(kv, "step") == 0, force_life = kv && strcmp(kv, "life") == 0;
-        e->life_lds = lds_bytes_life(e->NK, e->nkw, spec, c.key_window, c.variants);
         e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
+        e->life_lds = lds_bytes_life(e->NK, spec, c.key_window, c.variants, e->life_pl);
         e->life_rw = (e->life_pl && c.delay_max > 8) ? LIFE_RW16 : LIFE_RW;
         const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
                               c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
@@ -472,8 +472,7 @@ int brc_create(const brc_config* cfg, void** out) {
             return BRC_E_INVALID;
         }
     }
-    // narrow kernels: one lane clears one word of a ring row (act_types words per key word)
-    if ((e->step_ok && ((e->wide ? e->nkw > (uint32_t)e->nkw_t : e->nkw * act_types(e->compact) > 64) ||
+    if ((e->step_ok && ((e->wide && e->nkw > (uint32_t)e->nkw_t) ||
                         e->lds_bytes > 160 * 1024)) || e->nitems > 0x7FFFFFFFull * WPB) {
         g_create_err = "configuration exceeds the kernel's LDS / key-slot limits (lds " + std::to_string(e->lds_bytes) + " B)";
         delete e;
@@ -492,7 +491,7 @@ int brc_create(const brc_config* cfg, void** out) {
     struct A { void** p; size_t bytes; } allocs[] = {
         {(void**)&e->cells, e->life_cfg ? 8 : cells * (e->compact ? 4 : 8)}, {(void**)&e->meta, keys * 8}, {(void**)&e->mgen, keys * 4},
         {(void**)&e->kdst, keys * 8 * e->bw},
-        {(void**)&e->act, e->step_ok ? (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact) * 8 : 8},
+        {(void**)&e->act, e->step_ok ? (size_t)e->nitems * e->rs * e->nkw * act_types(e->compact, e->ipw) * 8 : 8},
         {(void**)&e->actany, (size_t)e->nitems * 4}, {(void**)&e->items, (size_t)e->nitems * sizeof(ItemState)},
         {(void**)&e->inst, c.instances * sizeof(InstState)}, {(void**)&e->istats, c.instances * 32},
         {(void**)&e->cons0, (size_t)e->nitems * e->lpi * 8}, {(void**)&e->cons1, (size_t)e->nitems * e->lpi * 8},

@@ -137,8 +137,9 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 
 // Activity-ring words per (row, key word): the lean kernels keep one ECHO and one READY row (typed
 // marks: a key step evaluates only the message types that can land; SEND arrivals are found from the
-// key metadata), the others one untyped row.
-__host__ __device__ constexpr uint32_t act_types(bool lean) { return lean ? 2u : 1u; }
+// key metadata), the others one untyped row per instance of the wave item (IPW = 64 / NPAD of them): each
+// instance walks its own key list, so a key step loads only the instances that have arrivals on it.
+__host__ __device__ constexpr uint32_t act_types(bool lean, uint32_t ipw = 1) { return lean ? 2u : ipw; }
 
 // Injection records the non-lean narrow kernels stage in LDS at a time (one memory round trip per
 // INJ_CACHE records instead of one per record: cfg3's equivocation pattern is 120 records per wave)
@@ -147,7 +148,8 @@ constexpr uint32_t INJ_CACHE = 16;
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][act_types][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u16 (not on the lean kernels) | klist[NK + 2 KPAD] u16 (tail padded with the trash row NK;
-// u32 entries on the lean REFERENCE / BEB kernels) | injc[INJ_CACHE][3] u64 (not on the lean kernels)
+// u32 entries on the lean REFERENCE / BEB kernels; one list per instance on the others) |
+// injc[INJ_CACHE][3] u64 (not on the lean kernels)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
     const uint32_t ipw = 64 / (uint32_t)npad;
@@ -155,11 +157,11 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t h_words = cons_words(spec, msize, Q, nv, value_ids(!lean));
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
-    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : 1u);
+    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : lean ? 1u : ipw);
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
     const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;
-    return 8 * (ipw * NK + rs * nkw * act_types(lean) + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4 +
+    return 8 * (ipw * NK + rs * nkw * act_types(lean, ipw) + dbits_words + h_words + l_words + gen_words + (klist_u16 + 3) / 4 +
                 injc_words);
 }
 
@@ -200,12 +202,11 @@ inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32
 
 // Key-lifetime kernel (brc_life.h): ring steps (> 4 Dd - 1 for Dd <= 8) and LDS bytes of one wave
 // (must match the kernel's carve):
-//   meta[NK] u32 | snap[NK] u16 (padded to 8 B) | dkA[RW][nkw] u64 | dkB[RW][nkw] u64 |
-//   ring[RW] {u64 arrivals | msgs, u64 cells | deliveries} | consensus area (cons_words at NPAD = 64) |
-//   pr[64] u32 (connection peers: READY copies per relative step and receiver class)
+//   meta[NK] u32 | two-class form: dA[NK], dB[NK] u16 (each receiver class's delivery step of the key) |
+//   consensus area (cons_words at NPAD = 64)
 constexpr uint32_t LIFE_RW = 32;
-__host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, uint32_t nkw, bool spec, uint32_t Q, uint32_t nv) {
-    return 4 * NK + ((2 * NK + 7) & ~7u) + 2 * LIFE_RW * nkw * 8 + LIFE_RW * 16 + 8 * cons_words(spec, 8, Q, nv) + 256;
+__host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, bool spec, uint32_t Q, uint32_t nv, bool perlink) {
+    return 4 * NK + (perlink ? 0u : 4 * NK) + 8 * cons_words(spec, 8, Q, nv);
 }
 // Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
 // (perlink: uniform / geometric delays, delivery bitmaps in P.dring; dm16: delays up to 16, whose

@@ -71,6 +71,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     static_assert(!(QBIG && (PL || MODE == BRC_MODE_SPEC)), "key windows above 32: two-class form, not SPEC");
     constexpr uint32_t RW = (PL && DLX > 8) ? 64u : LIFE_RW;     // ring rows (> the longest key lifetime)
     constexpr uint64_t RWM = RW == 64 ? ~0ull : ((1ull << RW) - 1ull);
+    // pending-step masks: bit r - PB <=> relative step r.  RW = 32: PB = 0 (steps <= 32 plus a delay <= 8
+    // stay inside 64 bits); RW = 64: PB = 1 (steps 1 .. 64), and a step past the ring is an overflow
+    constexpr uint32_t PB = RW == 64 ? 1u : 0u;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const uint32_t lane = threadIdx.x;
     const uint64_t item = blockIdx.x;
@@ -82,17 +85,14 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 
     // ---- LDS carve (lds_bytes_life)
     uint32_t* s_meta = (uint32_t*)smem;
-    uint16_t* s_snap = (uint16_t*)(s_meta + NK);
-    // two-class delivery rings (LIFE_RW rows; the per-link form keeps its deliveries in HBM, P.dring)
-    uint64_t* s_dkA = (uint64_t*)((char*)smem + 4 * NK + ((2 * NK + 7) & ~7u));
-    uint64_t* s_dkB = s_dkA + LIFE_RW * nkw;
-    uint64_t* s_ring = s_dkB + LIFE_RW * nkw;     // [row][2]: arrivals | msgs << 32, cells | deliveries << 32
-    uint64_t* s_hm = s_ring + 2 * LIFE_RW;        // REFERENCE / BEB: hosts per value [4][64]
+    // two-class form: the step at which each receiver class delivers key slot k (0xFFFF: not yet) -- a
+    // class's honest receivers evolve identically, so a class delivers a key once, at one step, whole.
+    // The per-link form keeps its deliveries in HBM (P.dring).
+    uint16_t* s_dA = (uint16_t*)(s_meta + NK);
+    uint16_t* s_dB = s_dA + NK;
+    uint64_t* s_hm = (uint64_t*)((char*)smem + 4 * NK + (PL ? 0u : 4 * NK));   // REFERENCE / BEB: hosts per value [4][64]
     uint64_t* s_seen = s_hm;                      // SPEC, NV > 1: [Q][64]
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));   // SPEC: [Q][64]
-    // CONN: READY copies landing at relative step r of the key being simulated, per receiver class:
-    // fast | slow << 16 (a lane may send several READY copies, at several steps: counts, not ballots)
-    uint32_t* s_pr = (uint32_t*)(s_hm + cons_words(SPEC, 8, Q, NV));
 
     const uint32_t d = lane;
     const uint64_t inst = item;                   // one instance per wave
@@ -169,8 +169,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     uint64_t* const dring = PL ? P.dring + item * (uint64_t)RW * nkw * 64 + lane : nullptr;
 
     // ---- LDS init
-    for (uint32_t i = lane; i < NK; i += 64) { s_meta[i] = 0; s_snap[i] = 0; }
-    for (uint32_t i = lane; i < 2 * LIFE_RW * nkw; i += 64) s_dkA[i] = 0;
+    for (uint32_t i = lane; i < NK; i += 64) {
+        s_meta[i] = 0;
+        if (!PL) { s_dA[i] = 0xFFFFu; s_dB[i] = 0xFFFFu; }
+    }
     if constexpr (SPEC) {
         for (uint32_t q = 0; q < Q; ++q) {
             if (seen_on) s_seen[q * 64 + lane] = 0;
@@ -206,8 +208,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     uint32_t msg_now = 0;                          // SEND messages sent this step (per lane, counted at once)
 
     // honest origin d broadcasts SEND for its key (d, s) with value v (core/byzantinerandomizedconsensus.py:48-50,
-    // :80-83, :102-106): the slot is claimed now, its lifetime is simulated after the step (simulate below)
-    auto send_key = [&](uint32_t s, uint32_t v) {
+    // :80-83, :102-106): the slot is claimed now, its lifetime is simulated after the step (simulate below).
+    // A reused slot's old delivery steps are <= now (reuse waits for its last arrival), so they match no
+    // later step: nothing of the old key needs clearing.
+    auto send_key_now = [&](uint32_t s, uint32_t v) {
         const uint32_t k = (d * NV) * Q + (s & Qm);
         const uint32_t m = s_meta[k];
         if ((lm_s1(m) != 0 && t < lm_tend(m)) || s >= 0x3FFEu) { ovf = true; return; }
@@ -221,6 +225,28 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         msg_now += n;
         st_smax = max(st_smax, s);
     };
+    // During the consensus pass a replica's SENDs are queued and made after it (as brc_step.h does): a phase
+    // change reuses the replica's own slot while another replica may still count this step's delivery of
+    // the slot's old key, so every slot's metadata stays as it was for the whole pass.  One replica's SENDs
+    // of one pass have consecutive phase indices: the first index and a 2-bit value each.
+    bool defer = false;
+    uint32_t sq_s = 0, sq_n = 0;
+    uint64_t sq_v = 0;
+    auto send_key = [&](uint32_t s, uint32_t v) {
+        if (defer) {
+            if (sq_n == 0) sq_s = s;
+            if (s == sq_s + sq_n && sq_n < 32u) { sq_v |= (uint64_t)(v & 3u) << (2 * sq_n); ++sq_n; }
+            else ovf = true;                             // cannot happen (consecutive indices, < 32 per step)
+            return;
+        }
+        send_key_now(s, v);
+    };
+    auto flush_sends = [&]() {
+        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (2 * i)) & 3u);
+        sq_n = 0; sq_v = 0;
+    };
+    // a slot's consensus view: value << 14 | (s + 1), as the BRB phase left it
+    auto snap = [&](uint32_t k) -> uint32_t { return s_meta[k] & 0xFFFFu; };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
             const uint32_t v = (order >> (2 * i)) & 3;
@@ -284,7 +310,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         }
     };
     auto spec_deliver = [&](uint32_t k) {
-        const uint32_t sn = s_snap[k];
+        const uint32_t sn = snap(k);
         const uint32_t s = (sn & 0x3FFFu) - 1u, v = sn >> 14, host = k >> ksh;
         const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
         if (s < cur) return;
@@ -307,18 +333,18 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t t0 = t;
         // SEND arrivals: fast receivers at 1 if the origin is fast, everyone else at Dd
         uint32_t sdl = (oF && laneF) ? 1u : Dd;
-        // relative steps with SEND / ECHO / READY arrivals: bit i <=> step i + 1 (steps 1 .. RW <= 64)
+        // relative steps with SEND / ECHO / READY arrivals: bit r - PB <=> step r
         uint64_t pendS = 0, pendE = 0, pendR = 0;
         if constexpr (PL) {
             sdl = 0;
 #pragma unroll
             for (int i = 0; i < DL; ++i) {
                 if ((L[i] >> o) & 1ull) sdl = (uint32_t)i + 1u;
-                if ((OV[i] >> o) & 1ull) pendS |= 1ull << i;
+                if ((OV[i] >> o) & 1ull) pendS |= (2ull >> PB) << i;
             }
         } else {
-            if (oF && HF) pendS |= 1ull;
-            if (HS || (!oF && HF)) pendS |= 1ull << (Dd - 1u);
+            if (oF && HF) pendS |= 2ull;
+            if (HS || (!oF && HF)) pendS |= 1ull << Dd;
         }
         uint32_t fl = 0, ec = 0, rc = 0, rE = LIFE_NEVER, rR = LIFE_NEVER;
         Ring16 ringR = {0ull, 0ull};                  // PL connection peers: READY copies per step
@@ -327,8 +353,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint32_t kw = k >> 6;
         const uint64_t kbit = 1ull << (k & 63);
         for (uint64_t pend = pendS; pend; pend = pendS | pendE | pendR) {
-            const uint32_t r = (uint32_t)__builtin_ctzll(pend) + 1u;
-            const uint64_t rb = 1ull << (r - 1u);
+            const uint32_t r = (uint32_t)__builtin_ctzll(pend) + PB;
+            const uint64_t rb = 1ull << (r - PB);
             const bool hS = (pendS & rb) != 0, hE = (pendE & rb) != 0, hR = (pendR & rb) != 0;
             pendS &= ~rb; pendE &= ~rb; pendR &= ~rb;
             if (r > RW) { ovf = true; break; }        // two-class: cannot happen for Dd <= 8 (lifetime <= 4 Dd)
@@ -493,8 +519,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 // receivers of one class evolve identically: a delivery step takes whole honest classes
                 const uint64_t dA = db & HF, dB = db & HS;
                 if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
-                if (dA && lane == 0) s_dkA[row * nkw + kw] |= kbit;
-                if (dB && lane == 0) s_dkB[row * nkw + kw] |= kbit;
+                if (dA && lane == 0) s_dA[k] = (uint16_t)ts;
+                if (dB && lane == 0) s_dB[k] = (uint16_t)ts;
             }
             // the messages sent now land on fast receivers after 1 step (fast senders) and on every
             // other (sender, receiver) pair after Dd steps
@@ -508,20 +534,19 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);
                     x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, true);
                     x = uni32(rl(x, 0) | rl(x, 16) | rl(x, 32) | rl(x, 48));
-                    // arrivals at r + i + 1 for every delay bit i: bit r + i (past the ring: overflow, never lost)
+                    // arrivals at r + i + 1 for every delay bit i: bit r + i + 1 - PB (RW = 64: a step past the
+                    // ring is an overflow, never lost; RW = 32: r <= 32 and delays <= 8 fit the 64 bits)
                     constexpr uint32_t DM1 = (1u << DL) - 1u;
-                    if (r + hibit(x & DM1) > RW || r + hibit(x >> DL) > RW) ovf = true;
-                    pendE |= (uint64_t)(x & DM1) << r;
-                    pendR |= (uint64_t)(x >> DL) << r;
+                    if (PB && (r + hibit(x & DM1) > RW || r + hibit(x >> DL) > RW)) ovf = true;
+                    pendE |= (uint64_t)(x & DM1) << (r + 1u - PB);
+                    pendR |= (uint64_t)(x >> DL) << (r + 1u - PB);
                 }
             } else if (eb) {
-                if (r + Dd > RW) ovf = true;
                 if ((eb & Fm) && HF) pendE |= rb << 1;
                 if (HS || ((eb & Sm) && HF)) pendE |= rb << Dd;
             }
             if (!PL && rbm) {
                 const bool at1 = cF && HF, atD = HS || (cS && HF);
-                if (r + Dd > RW) ovf = true;
                 if (at1) pendR |= rb << 1;
                 if (atD) pendR |= rb << Dd;
                 if constexpr (CONN) {
@@ -599,8 +624,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             if (ce) t_stop = t;
         }
         // ================= consensus: this step's deliveries in canonical (kp, s) order
-        for (uint32_t i = lane; i < NK; i += 64) s_snap[i] = (uint16_t)s_meta[i];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        defer = true;
         // this step's delivery bits of key word w for this lane (read once: PL clears the ring word)
         auto dword = [&](uint32_t w) -> uint64_t {
             uint64_t bits;
@@ -610,7 +634,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 if (bits) __hip_atomic_store(dp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (!cons_lane) bits = 0;
             } else {
-                const uint64_t kA = s_dkA[row * nkw + w], kB = s_dkB[row * nkw + w];
+                // the keys of word w whose delivery step for this lane's class is now
+                const uint32_t kk = w * 64 + lane;
+                const uint64_t kA = __ballot(s_dA[kk] == t), kB = __ballot(s_dB[kk] == t);
                 bits = cons_lane ? (laneF ? kA : kB) : 0ull;
             }
             return bits;
@@ -628,12 +654,12 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     for (uint32_t j = 0; j < wpg; ++j)
                         for (uint64_t x = gb[j]; x; x &= x - 1) {
                             const uint32_t kk = (w + j) * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1u;
-                            const uint32_t s1 = s_snap[kk] & 0x3FFFu;
+                            const uint32_t s1 = snap(kk) & 0x3FFFu;
                             if (s1 < bs) { bs = s1; bk = kk; }
                         }
                     gb[(bk >> 6) - w] &= ~(1ull << (bk & 63));
                     if constexpr (SPEC) spec_deliver(bk);
-                    else cons_deliver_vh((uint32_t)s_snap[bk] >> 14, bk >> ksh);
+                    else cons_deliver_vh(snap(bk) >> 14, bk >> ksh);
                 }
             }
         } else
@@ -648,7 +674,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     const uint32_t cur = round ? 2 * (round - 1) + (phase - 1) : 0u;
                     const uint32_t c0 = uni32((uint32_t)__builtin_amdgcn_readlane((int)cur, __ffsll((unsigned long long)hb) - 1));
                     if (!__ballot(bits != 0 && cur != c0)) {
-                        const uint32_t sn = s_snap[w * 64 + lane];
+                        const uint32_t sn = snap(w * 64 + lane);
                         const uint32_t ss = (sn & 0x3FFFu) - 1u, sv = sn >> 14;
                         const uint64_t inw = __ballot(ss >= c0 && ss - c0 < Q), atc = __ballot(ss == c0);
                         const uint64_t past = __ballot(ss != 0xFFFFFFFFu && ss >= c0 && ss - c0 >= Q);
@@ -672,7 +698,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             } else {
                 // word at once when no phase can change (brc_step.h, REFERENCE consensus pass)
                 if (__ballot(bits != 0)) {
-                    const uint32_t sv = (uint32_t)s_snap[w * 64 + lane] >> 14;
+                    const uint32_t sv = snap(w * 64 + lane) >> 14;
                     const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
                     const uint32_t nb = (uint32_t)__popcll(bits);
                     const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
@@ -709,20 +735,22 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     uint32_t bs = 0xFFFFFFFFu;
                     for (uint64_t x = grp; x; x &= x - 1) {
                         const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                        const uint32_t s1 = s_snap[w * 64 + bb] & 0x3FFFu;
+                        const uint32_t s1 = snap(w * 64 + bb) & 0x3FFFu;
                         if (s1 < bs) { bs = s1; best = bb; }
                     }
                 }
                 bits &= ~(1ull << best);
                 if constexpr (SPEC) spec_deliver(w * 64 + best);
-                else cons_deliver_vh((uint32_t)s_snap[w * 64 + best] >> 14, (w * 64 + best) >> ksh);
+                else cons_deliver_vh(snap(w * 64 + best) >> 14, (w * 64 + best) >> ksh);
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        defer = false;
+        flush_sends();                                // the SENDs this step's consensus started
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         acc_add(0u, wave_sum(msg_now));
         msg_now = 0;
         // the step is consumed: its ring row is free for step t + RW
-        for (uint32_t i = lane; i < 2 * nkw; i += 64) (i < nkw ? s_dkA : s_dkB)[row * nkw + (i % nkw)] = 0;
         if (lane == row) { rg_arr = 0; rg_msg = 0; rg_cell = 0; rg_del = 0; }
         rows &= ~((RowT)1 << row);
         // ================= per-instance stop conditions (brc_step.h)

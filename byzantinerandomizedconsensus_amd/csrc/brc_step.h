@@ -414,7 +414,9 @@ void brc_step(const Params* __restrict__ pp) {
     using T = typename MaskOf<NPAD>::type;
     constexpr uint32_t RS = ring_steps(DM);      // activity-ring rows (> the largest delay)
     constexpr int IPW = 64 / NPAD;
-    constexpr uint32_t AT = act_types(LEAN);     // activity-ring words per (row, key word)
+    // activity-ring words per (row, key word): lean, one per message type; else one per instance of the item
+    constexpr uint32_t AT = act_types(LEAN, IPW);
+    constexpr bool PSEG = !LEAN && IPW > 1;       // each instance of the item walks its own key list
     // consensus value ids (brc_internal.h value_ids): VB bits each, NVAL of them; VREP has a 1 in
     // the low bit of every VB-bit field of `order`
     constexpr uint32_t NVAL = value_ids(!LEAN), VB = LEAN ? 2u : 3u, VMASK = NVAL - 1u;
@@ -451,11 +453,12 @@ void brc_step(const Params* __restrict__ pp) {
     // gen | GEN16_RESTRICTED (lean kernels keep no generations: no area)
     uint16_t* s_gen = (uint16_t*)(s_dbits + dbw + h_words + l_words);
     uint16_t* s_klist = s_gen + (LEAN ? 0u : ((IPW * NK + 3) & ~3u));        // this step's active key slots
+    const uint32_t KLS = NK + 2 * KPAD;          // PSEG: entries per instance list (list seg at seg * KLS)
     // lean REFERENCE / BEB: u32 entries (KL_*); lean SPEC keeps u16 entries (its LDS bounds its residency)
     constexpr bool KL32 = LEAN && (!SPEC || BRC_KL32_SPEC);
     uint32_t* s_klist32 = (uint32_t*)s_klist;
     // non-lean kernels: a window of the item's injection records, staged in LDS (INJ_CACHE at a time)
-    uint64_t* s_injc = (uint64_t*)(s_klist + ((NK + 2 * KPAD + 3) & ~3u));
+    uint64_t* s_injc = (uint64_t*)(s_klist + ((KLS * (PSEG ? IPW : 1u) + 3) & ~3u));
 
     const int seg = lane / NPAD, d = lane % NPAD, segbase = seg * NPAD;
     const uint64_t inst = item * IPW + seg;
@@ -717,7 +720,7 @@ void brc_step(const Params* __restrict__ pp) {
             const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
             const uint32_t row = (t + i + 1) & (RS - 1);
             if (!LEAN || ty != BRC_SEND)
-                atomicOr((unsigned long long*)&s_act[(row * AT + (LEAN ? ty - BRC_ECHO : 0u)) * nkw + (k >> 6)],
+                atomicOr((unsigned long long*)&s_act[(row * AT + (LEAN ? ty - BRC_ECHO : (uint32_t)seg)) * nkw + (k >> 6)],
                          1ull << (k & 63));
             lane_rows |= 1u << row;
         }
@@ -1133,7 +1136,7 @@ void brc_step(const Params* __restrict__ pp) {
             else s_dbits[wk * 64 + lane] = v;
             dwm |= 1u << wk;
         };
-        uint32_t nkeys = 0;
+        uint32_t nkeys = 0, nks = 0;                // PSEG: nks = this instance's list length
         if constexpr (LEAN) {
             // typed marks: ECHO / READY rows; SEND arrivals from the slot's metadata -- the SEND of slot
             // k lands now at some receiver iff t - t_send is a delay of its sender's outset (reading the
@@ -1167,6 +1170,19 @@ void brc_step(const Params* __restrict__ pp) {
                 }
                 nkeys += (uint32_t)__popcll(bits);
             }
+        } else if constexpr (PSEG) {
+            // one key list per instance (segment): the segment's lanes list its marked slots, NPAD bits
+            // of a ring word at a time; nks = this segment's length, nkeys = the longest list
+            for (uint32_t w = 0; w < nkw; ++w) {
+                const uint64_t bits = s_act[(row * AT + (uint32_t)seg) * nkw + w];
+                for (uint32_t b0 = 0; b0 < 64; b0 += NPAD) {
+                    const uint32_t b = b0 + (uint32_t)d;
+                    if ((bits >> b) & 1ull)
+                        s_klist[(uint32_t)seg * KLS + nks + (uint32_t)__popcll(bits & ((1ull << b) - 1ull))] = (uint16_t)(w * 64 + b);
+                }
+                nks += (uint32_t)__popcll(bits);
+            }
+            nkeys = wave_max_all(nks);
         } else {
             for (uint32_t w = 0; w < nkw; ++w) {
                 const uint64_t bits = uni64(s_act[row * nkw + w]);
@@ -1176,7 +1192,7 @@ void brc_step(const Params* __restrict__ pp) {
                 nkeys += (uint32_t)__popcll(bits);
             }
         }
-        if (lane < 2 * KPAD) {                                    // chunk padding -> the trash row
+        if (!PSEG && lane < 2 * KPAD) {                           // chunk padding -> the trash row
             if constexpr (KL32) s_klist32[nkeys + lane] = NK;
             else s_klist[nkeys + lane] = (uint16_t)NK;
         }
@@ -1188,7 +1204,12 @@ void brc_step(const Params* __restrict__ pp) {
         auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK], uint32_t (&kk)[CHUNK]) {
             Unrolled<CHUNK>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
-                kk[c] = uni32(s_klist[p + c]);
+                if constexpr (PSEG) {
+                    // this instance's own list (past its end: the trash row), one key per segment
+                    kk[c] = p + c < nks ? (uint32_t)s_klist[(uint32_t)seg * KLS + p + c] : NK;
+                } else {
+                    kk[c] = uni32(s_klist[p + c]);
+                }
                 ww[c] = mycells[(size_t)kk[c] * (CW * 64)];
             });
         };
@@ -1637,10 +1658,19 @@ void brc_step(const Params* __restrict__ pp) {
                     if (IPW > 1 && ((x & segbits) != 0)) oss |= 1u << i;
                 }
                 if (IPW == 1) oss = os;
-                for (uint32_t x = os; x; x &= x - 1) {
-                    const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
-                    if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
-                    any_rows |= 1u << r;
+                if constexpr (PSEG) {
+                    // the key is this segment's (keys differ across segments): its own senders' delays
+                    for (uint32_t x = oss; x; x &= x - 1) {
+                        const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
+                        if (d == 0) atomicOr((unsigned long long*)&s_act[(r * AT + (uint32_t)seg) * nkw + (k >> 6)], 1ull << (k & 63));
+                        lane_rows |= 1u << r;
+                    }
+                } else {
+                    for (uint32_t x = os; x; x &= x - 1) {
+                        const uint32_t r = (t + (uint32_t)__ffs(x)) & (RS - 1);
+                        if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));
+                        any_rows |= 1u << r;
+                    }
                 }
                 const uint32_t myq = oss ? t + hibit(oss) : 0u;
                 if (live && myq) {
@@ -1993,7 +2023,7 @@ void brc_step(const Params* __restrict__ pp) {
             else if (P.protocol == BRC_PROTO_CONSENSUS && P.round_cap > 0 && !b_und) status = BRC_DONE;
             else if (q_until <= t && !((seg_pending >> seg) & 1u)) status = BRC_QUIESCENT;
         }
-        if ((uint32_t)lane < nkw * AT) s_act[row * nkw * AT + lane] = 0;
+        for (uint32_t i = lane; i < nkw * AT; i += 64) s_act[row * nkw * AT + i] = 0;
         any_rows &= ~(1u << row);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         BRC_STAMP(4);

@@ -9,6 +9,7 @@
 #   configs[=<names>]             configs.py [--only names]                  -> configs.jsonl
 #   collect=<ptag>,<inst>,<leg>,<kernel>[,<passes>]   profiles/collect.sh    -> collect_<ptag>.log
 #   ab=<tags>,<rounds>[,<bench args>]                 tools/ab.sh            -> ab.log
+#   abcfg=<tags>,<rounds>,<configs names>             tools/ab_cfg.sh        -> abcfg.log
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -35,6 +36,10 @@ for step in "$@"; do
     ab)
       IFS=, read -r tags rounds bargs <<< "$arg"
       timeout -k 10 1200 bash tools/ab.sh "$tags" $rounds $bargs > $OUT/ab.log 2>&1; rc=$?; cat $OUT/ab.log ;;
+    abcfg)
+      IFS=, read -r tags rounds names <<< "$arg"
+      names=${names//+/,}
+      timeout -k 10 1200 bash tools/ab_cfg.sh "$tags" $rounds $names > $OUT/abcfg.log 2>&1; rc=$?; cat $OUT/abcfg.log ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
   if [ $rc -ne 0 ]; then echo "step $step failed: rc $rc"; exit $rc; fi

@@ -9,6 +9,6 @@ rm -rf $WT; git -C $ROOT worktree prune
 git -C $ROOT worktree add --detach $WT $REV >/dev/null
 python3 $WT/tools/variant.py $TAG "$@" >/dev/null
 mkdir -p $ROOT/ab/$TAG
-cp $WT/ab/$TAG/libbrc_hip.so $ROOT/ab/$TAG/libbrc_hip.so
+cp $WT/ab/$TAG/libbrc_hip.so $ROOT/ab/$TAG/libbrc_hip.so 2>/dev/null || cp $WT/exp/$TAG/libbrc_hip.so $ROOT/ab/$TAG/libbrc_hip.so   # revisions before round 5 build into exp/
 git -C $ROOT worktree remove --force $WT
 echo $ROOT/ab/$TAG/libbrc_hip.so

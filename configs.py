@@ -16,12 +16,15 @@ Workloads:
   cfg4-conn  the same with connection-identity peers (what the shipped reference runs), 2^20
   cfg4-conn-uniform[-d2]  connection peers under per-link uniform[1,4] ([1,2]) delays, 2^20
   cfg4-beb   the reference consensus over best-effort broadcast (BRC_MODE_BEB), 2^20
+  cfg4-ref-r8  the reference protocol to round cap 8 (bench.py's many leg: the key-lifetime kernel), 2^20
+  cfg4-conn-geometric  connection peers under geometric delays capped at 16 (64-row ring), 2^20
   cfg5-*     n=256 f=85 SPEC, 6144 instances per GPU, const / uniform[1,4] / geometric<=16
 
 A step is one pass of the hot path over the batch (reset + run to completion); the timed region
 is K steps between barriers, max over ranks.  `roofline.achieved` = this layout's algorithmic
 bytes (the cell word read + written, 2 x cell bytes per cell-step) x cell-steps per launch /
-kernel time; `survey_model_frac` prices SURVEY §8(d)'s 6*ceil(n/8)+2 B per cell-step instead.
+kernel time; `survey_model_gbs` prices SURVEY §8(d)'s 6*ceil(n/8)+2 B per cell-step instead;
+`traffic_frac` and `issue` come from the workload's committed same-build rocprofv3 profile.
 """
 import argparse
 import json
@@ -70,6 +73,12 @@ def workloads(L):
                                 key_window=4, peer_mode=L.PEER_CONNECTION))
     W["cfg4-beb"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                          round_cap=1, key_window=8, mode=L.MODE_BEB))
+    # the reference protocol to round cap 8 (bench.py's many leg; the key-lifetime kernel at 2^20)
+    W["cfg4-ref-r8"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                            round_cap=8, key_window=32))
+    # connection peers under cfg5's geometric delays capped at 16 (the per-link form's 64-row ring)
+    W["cfg4-conn-geometric"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=3, delay_max=16,
+                                                    round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
         # 6,144 instances per GPU: 8 waves of the 768 resident workgroups (3 per CU), so no partial last wave
         W["cfg5-" + name] = (6144, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
@@ -86,23 +95,46 @@ def cell_bytes(n, peer_mode=0):
     return 4 if 32 < n <= 64 else 8
 
 
-def measured_traffic(name, kernel_ms):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of this workload
-    (profiles/*/pmc_traffic.json written by profiles/summarize.py), if its kernel time agrees
-    with the live one within 15 % (the same kernel build)."""
+# configs.py workloads that are bench.py legs: their profiles are the bench's (workload "cfg4", mode = leg)
+BENCH_LEGS = {"cfg4-ref": "reference", "cfg4-spec": "spec", "cfg4-conn": "conn", "cfg4-conn-uniform-d2": "connu",
+              "cfg4-ref-r8": "many"}
+
+
+def measured_profile(name, kernel_ms):
+    """The committed rocprofv3 summary of this workload (profiles/*/pmc_traffic.json, written by
+    profiles/summarize.py from a configs.py --only <name> run, or the bench.py leg's for the cfg4
+    workloads that are bench legs): HBM bytes per launch and the issue block, if its kernel time
+    agrees with the live one within 15 % (the same kernel build).  The newest matching profile wins."""
     import glob
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json"))):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")),
+                       key=lambda p: os.path.getmtime(p)):
         try:
             with open(path) as fh:
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if d.get("workload") != name or not d.get("avg_ns") or not d.get("hbm_bytes_per_launch"):
+        mine = d.get("workload") == name or (name in BENCH_LEGS and d.get("workload") == "cfg4" and
+                                               d.get("mode", "reference") == BENCH_LEGS[name] and
+                                               d.get("instances") == 1 << 20)
+        if not mine or not d.get("avg_ns") or not d.get("hbm_bytes_per_launch"):
             continue
         if abs(d["avg_ns"] / 1e6 - kernel_ms) <= 0.15 * kernel_ms:
-            best = (d["hbm_bytes_per_launch"], os.path.relpath(path, ROOT))
+            best = dict(d, path=os.path.relpath(path, ROOT))
     return best
+
+
+def attach_profile(out, name, kernel_ms):
+    prof = measured_profile(name, kernel_ms)
+    if prof:
+        sec = kernel_ms / 1e3
+        out["traffic"], out["traffic_source"] = prof["hbm_bytes_per_launch"], prof["path"]
+        out["traffic_frac"] = prof["hbm_bytes_per_launch"] / sec / 1e9 / HBM_PEAK_GBS
+        out["profile"] = {"source": prof["path"], "kernel_ms": prof["avg_ns"] / 1e6,
+                          "agreement": prof["avg_ns"] / 1e6 / kernel_ms}
+        if prof.get("issue"):
+            out["issue"] = prof["issue"]
+    return out
 
 
 def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0, kernel="step"):
@@ -116,31 +148,23 @@ def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0, kernel="step"):
         raise ValueError("%s: launches ran different kernels (%r); report them apart" % (name, kernel))
     if kernel == "life":
         out = {"bound": "issue", "kernel": "brc_life", "unit": "GB/s", "peak": HBM_PEAK_GBS, "achieved": None,
-               "frac": None, "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS,
+               "frac": None, "survey_model_gbs": bpc * cell_steps / sec / 1e9,
                "cell_steps_per_s": cell_steps / sec, "traffic": None, "traffic_frac": None,
                "note": "key-lifetime kernel: cells stay in registers for a key's lifetime, no HBM cell traffic "
                        "(per-link form: one 8-B delivery-bitmap word per lane, key word and step in HBM); "
-                       "survey_model_frac prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
-        t = measured_traffic(name, kernel_ms)
-        if t:
-            out["traffic"], out["traffic_source"] = t
-            out["traffic_frac"] = t[0] / sec / 1e9 / HBM_PEAK_GBS
-        return out
+                       "survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
+        return attach_profile(out, name, kernel_ms)
     floor_b = 2 * cell_bytes(n, peer_mode)
     achieved = floor_b * cell_steps / sec / 1e9
     out = {"bound": "hbm", "kernel": "brc_step" if n <= 64 else "brc_step_wide", "unit": "GB/s", "peak": HBM_PEAK_GBS,
            "achieved": achieved,
            "frac": achieved / HBM_PEAK_GBS, "bytes_per_unit": floor_b,
-           "survey_model_frac": bpc * cell_steps / sec / 1e9 / HBM_PEAK_GBS, "cell_bytes": floor_b // 2,
+           "survey_model_gbs": bpc * cell_steps / sec / 1e9, "cell_bytes": floor_b // 2,
            "traffic": None, "traffic_frac": None,
-           "note": "achieved: %d B per cell-step (the %d-B cell read + written); survey_model_frac prices SURVEY "
-                   "8(d)'s %d B at n=%d, which credits n-bit sets this layout never moves, so it can pass 1; "
-                   "traffic_frac: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE" % (floor_b, floor_b // 2, bpc, n)}
-    t = measured_traffic(name, kernel_ms)
-    if t:
-        out["traffic"], out["traffic_source"] = t
-        out["traffic_frac"] = t[0] / sec / 1e9 / HBM_PEAK_GBS
-    return out
+           "note": "achieved: %d B per cell-step (the %d-B cell read + written); survey_model_gbs prices SURVEY "
+                   "8(d)'s %d B at n=%d, which credits n-bit sets this layout never moves (it can exceed the "
+                   "peak); traffic_frac: rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE" % (floor_b, floor_b // 2, bpc, n)}
+    return attach_profile(out, name, kernel_ms)
 
 
 def main():

@@ -1586,8 +1586,11 @@ void brc_step(const Params* __restrict__ pp) {
             const bool s_win = kl && dt - 1u < D && (dset & bit) != 0;     // uniform if IPW == 1
             if (IPW == 1 ? s_win : __any(s_win)) {
                 bool hit = (Lmask(popc(dset & (bit - 1u))) >> m_sender(m)) & 1;
-                if (IPW == 1 ? (gw & GEN16_RESTRICTED) != 0 : __any((gw & GEN16_RESTRICTED) != 0))
-                    hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
+                // a restricted SEND lands only on its destinations (kdst); per lane -- the lanes of an item hold
+                // different instances, each its own key (and padding lanes, whose slot fields are junk)
+                const bool restr = s_win && (gw & GEN16_RESTRICTED) != 0;
+                if (IPW == 1 ? restr : __any(restr))
+                    if (restr) hit = hit && ((gp(P.kdst)[inst * NK + k] >> d) & 1ull);
                 s_arr = s_win && hon_run && hit;
             }
             const uint32_t sa = (LEAN ? 0u : xsa) + (s_arr ? 1u : 0u);   // SEND arrivals (extra SENDs: several)

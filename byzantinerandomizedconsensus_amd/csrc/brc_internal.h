@@ -137,9 +137,14 @@ __host__ __device__ inline uint32_t cons_words(bool spec, uint32_t msize, uint32
 
 // Activity-ring words per (row, key word): the lean kernels keep one ECHO and one READY row (typed
 // marks: a key step evaluates only the message types that can land; SEND arrivals are found from the
-// key metadata), the others one untyped row per instance of the wave item (IPW = 64 / NPAD of them): each
-// instance walks its own key list, so a key step loads only the instances that have arrivals on it.
-__host__ __device__ constexpr uint32_t act_types(bool lean, uint32_t ipw = 1) { return lean ? 2u : ipw; }
+// key metadata), the others one untyped row for the wave item.  BRC_PSEG=1 (experimental) gives the
+// non-lean kernels one row and key list per instance of the item (IPW = 64 / NPAD of them), so a key
+// step loads only the instances with arrivals on it: measured SLOWER on cfg2 / cfg3 / cfg3-spec /
+// cfg2-spec (per-lane key ids turn the key dispatch into vector work; round-5 A/B), so off by default.
+#ifndef BRC_PSEG
+#define BRC_PSEG 0
+#endif
+__host__ __device__ constexpr uint32_t act_types(bool lean, uint32_t ipw = 1) { return lean ? 2u : BRC_PSEG ? ipw : 1u; }
 
 // Injection records the non-lean narrow kernels stage in LDS at a time (one memory round trip per
 // INJ_CACHE records instead of one per record: cfg3's equivocation pattern is 120 records per wave)
@@ -148,7 +153,7 @@ constexpr uint32_t INJ_CACHE = 16;
 // Bytes of dynamic LDS one wave of the step kernel needs (must match the kernel's carve):
 // meta[IPW*NK] u64 | act[RS][act_types][nkw] u64 | dbits[nkw][64] u64 (not on lean SPEC) | consensus area | L[nL][64] T |
 // mgen[IPW*NK] u16 (not on the lean kernels) | klist[NK + 2 KPAD] u16 (tail padded with the trash row NK;
-// u32 entries on the lean REFERENCE / BEB kernels; one list per instance on the others) |
+// u32 entries on the lean REFERENCE / BEB kernels; BRC_PSEG: one list per instance on the others) |
 // injc[INJ_CACHE][3] u64 (not on the lean kernels)
 __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec,
                                                        uint32_t Q, uint32_t nv, uint32_t rs, bool lean) {
@@ -157,7 +162,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
     const uint32_t h_words = cons_words(spec, msize, Q, nv, value_ids(!lean));
     const uint32_t l_words = (nL * 64 * msize + 7) / 8;
     // (lean REFERENCE / BEB kernels: u32 entries, brc_step.h KL_*)
-    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : lean ? 1u : ipw);
+    const uint32_t klist_u16 = (NK + 2 * KPAD) * ((lean && (!spec || BRC_KL32_SPEC)) ? 2u : lean ? 1u : act_types(false, ipw));
     const uint32_t gen_words = lean ? 0u : (ipw * NK + 3) / 4;   // lean kernels keep no slot generations
     const uint32_t dbits_words = (lean && spec) ? 0u : 64 * nkw;   // lean SPEC keeps them in HBM
     const uint32_t injc_words = lean ? 0u : 3 * INJ_CACHE;

@@ -416,7 +416,7 @@ void brc_step(const Params* __restrict__ pp) {
     constexpr int IPW = 64 / NPAD;
     // activity-ring words per (row, key word): lean, one per message type; else one per instance of the item
     constexpr uint32_t AT = act_types(LEAN, IPW);
-    constexpr bool PSEG = !LEAN && IPW > 1;       // each instance of the item walks its own key list
+    constexpr bool PSEG = BRC_PSEG && !LEAN && IPW > 1;   // each instance walks its own key list
     // consensus value ids (brc_internal.h value_ids): VB bits each, NVAL of them; VREP has a 1 in
     // the low bit of every VB-bit field of `order`
     constexpr uint32_t NVAL = value_ids(!LEAN), VB = LEAN ? 2u : 3u, VMASK = NVAL - 1u;
@@ -720,7 +720,7 @@ void brc_step(const Params* __restrict__ pp) {
             const uint32_t i = __ffs(ds) - 1; ds &= ds - 1;
             const uint32_t row = (t + i + 1) & (RS - 1);
             if (!LEAN || ty != BRC_SEND)
-                atomicOr((unsigned long long*)&s_act[(row * AT + (LEAN ? ty - BRC_ECHO : (uint32_t)seg)) * nkw + (k >> 6)],
+                atomicOr((unsigned long long*)&s_act[(row * AT + (LEAN ? ty - BRC_ECHO : PSEG ? (uint32_t)seg : 0u)) * nkw + (k >> 6)],
                          1ull << (k & 63));
             lane_rows |= 1u << row;
         }

@@ -207,11 +207,11 @@ inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32
 
 // Key-lifetime kernel (brc_life.h): ring steps (> 4 Dd - 1 for Dd <= 8) and LDS bytes of one wave
 // (must match the kernel's carve):
-//   meta[NK] u32 | two-class form: dA[NK], dB[NK] u16 (each receiver class's delivery step of the key) |
-//   consensus area (cons_words at NPAD = 64)
+//   meta[NK] u32 | two-class form: dA[NK], dB[NK] u8 (each receiver class's delivery step of the key,
+//   0x80 | step mod 128) | (8-B aligned) consensus area (cons_words at NPAD = 64)
 constexpr uint32_t LIFE_RW = 32;
 __host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, bool spec, uint32_t Q, uint32_t nv, bool perlink) {
-    return 4 * NK + (perlink ? 0u : 4 * NK) + 8 * cons_words(spec, 8, Q, nv);
+    return ((4 * NK + (perlink ? 0u : 2 * NK) + 7) & ~7u) + 8 * cons_words(spec, 8, Q, nv);
 }
 // Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
 // (perlink: uniform / geometric delays, delivery bitmaps in P.dring; dm16: delays up to 16, whose

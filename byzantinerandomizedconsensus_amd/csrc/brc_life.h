@@ -85,12 +85,15 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 
     // ---- LDS carve (lds_bytes_life)
     uint32_t* s_meta = (uint32_t*)smem;
-    // two-class form: the step at which each receiver class delivers key slot k (0xFFFF: not yet) -- a
-    // class's honest receivers evolve identically, so a class delivers a key once, at one step, whole.
-    // The per-link form keeps its deliveries in HBM (P.dring).
-    uint16_t* s_dA = (uint16_t*)(s_meta + NK);
-    uint16_t* s_dB = s_dA + NK;
-    uint64_t* s_hm = (uint64_t*)((char*)smem + 4 * NK + (PL ? 0u : 4 * NK));   // REFERENCE / BEB: hosts per value [4][64]
+    // two-class form: the step at which each receiver class delivers key slot k -- a class's honest
+    // receivers evolve identically, so a class delivers a key once, at one step, whole.  One byte,
+    // 0x80 | step mod 128 (0: none): a key's deliveries lie within 4 Dd <= 32 steps of its creation, and
+    // the consensus pass clears the entries of the step it consumes (every entry's step is one it visits:
+    // a delivery lands on an honest class, so its step has arrivals), so no stale entry aliases a later
+    // step.  The per-link form keeps its deliveries in HBM (P.dring).
+    uint8_t* s_dA = (uint8_t*)(s_meta + NK);
+    uint8_t* s_dB = s_dA + NK;
+    uint64_t* s_hm = (uint64_t*)((char*)smem + ((4 * NK + (PL ? 0u : 2 * NK) + 7) & ~7u));   // REFERENCE / BEB: hosts per value [4][64]
     uint64_t* s_seen = s_hm;                      // SPEC, NV > 1: [Q][64]
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));   // SPEC: [Q][64]
 
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) {
         s_meta[i] = 0;
-        if (!PL) { s_dA[i] = 0xFFFFu; s_dB[i] = 0xFFFFu; }
+        if (!PL) { s_dA[i] = 0; s_dB[i] = 0; }
     }
     if constexpr (SPEC) {
         for (uint32_t q = 0; q < Q; ++q) {
@@ -519,8 +522,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 // receivers of one class evolve identically: a delivery step takes whole honest classes
                 const uint64_t dA = db & HF, dB = db & HS;
                 if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
-                if (dA && lane == 0) s_dA[k] = (uint16_t)ts;
-                if (dB && lane == 0) s_dB[k] = (uint16_t)ts;
+                if (dA && lane == 0) s_dA[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
+                if (dB && lane == 0) s_dB[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
             }
             // the messages sent now land on fast receivers after 1 step (fast senders) and on every
             // other (sender, receiver) pair after Dd steps
@@ -635,8 +638,13 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 if (!cons_lane) bits = 0;
             } else {
                 // the keys of word w whose delivery step for this lane's class is now
-                const uint32_t kk = w * 64 + lane;
-                const uint64_t kA = __ballot(s_dA[kk] == t), kB = __ballot(s_dB[kk] == t);
+                const uint32_t kk = w * 64 + lane, tc = 0x80u | (t & 0x7Fu);
+                const uint32_t eA = s_dA[kk], eB = s_dB[kk];
+                const uint64_t kA = __ballot(eA == tc), kB = __ballot(eB == tc);
+                if (kA | kB) {                            // consumed: free the entries for step t + 128
+                    if (eA == tc) s_dA[kk] = 0;
+                    if (eB == tc) s_dB[kk] = 0;
+                }
                 bits = cons_lane ? (laneF ? kA : kB) : 0ull;
             }
             return bits;

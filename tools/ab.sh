@@ -11,6 +11,6 @@ for r in $(seq 1 $ROUNDS); do
   for t in $TAGS; do
     if [ "$t" = head ]; then lib=""; else lib=ab/$t/libbrc_hip.so; fi
     BRC_LIB=$lib timeout -k 10 300 python3 bench.py $ARGS > gpurun_out/ab/$t.$r.json 2> gpurun_out/ab/$t.$r.err || { echo "FAIL $t round $r"; tail -5 gpurun_out/ab/$t.$r.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['kernel_ms'],2), round(d['value']/1e6,3), d['decided_fraction'])" gpurun_out/ab/$t.$r.json $t
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['kernel_ms'],2), round(d['value']/1e6,3), d['decided_fraction'], {k[:-4]: round(v['kernel_ms'],2) for k, v in d.items() if k.endswith('_leg')})" gpurun_out/ab/$t.$r.json $t
   done
 done

@@ -144,13 +144,14 @@ struct Engine {
     brc_config cfg;
     int npad = 0, dm = 0, ipw = 0, nkw_t = 0;
     bool wide = false;                           // n > 64: one workgroup per instance (brc_step_wide.h)
+    bool wide_wv4 = false;                       // wide: the 4-waves-per-SIMD instantiations (brc_step_wide.h WV)
     bool regmask = false;                        // NPAD = 64 lean kernel with register delay masks (NLR = 2)
     bool compact = false;                        // lean kernels (NPAD = 64, sender peers): u32 cells (C32_*)
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
     uint32_t rows = 0;                           // cell rows per item
-    uint32_t rs = TS;                            // activity-ring rows (narrow kernel: ring_steps(dm))
+    uint32_t rs = TS;                            // activity-ring rows: ring_steps(dm)
     uint64_t cons_bytes = 0;                     // consensus-set buffer (hmask) bytes per item
     uint64_t nitems = 0;
     hipStream_t stream = nullptr;
@@ -221,7 +222,7 @@ static uint64_t word_mask(uint32_t n, uint32_t w) {
 
 static int pick_dm(uint32_t d) { return d <= 4 ? 4 : d <= 8 ? 8 : 16; }
 
-static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t st,
+static int launch_step(int npad, int dm, bool events, int mode, bool wv4, uint32_t blocks, uint32_t lds, hipStream_t st,
                        const Params* P) {
     switch (npad) {
     case 4: return launch_step_4(dm, events, mode, blocks, lds, st, P);
@@ -229,8 +230,8 @@ static int launch_step(int npad, int dm, bool events, int mode, uint32_t blocks,
     case 16: return launch_step_16(dm, events, mode, blocks, lds, st, P);
     case 32: return launch_step_32(dm, events, mode, blocks, lds, st, P);
     case 64: return launch_step_64(dm, events, mode, blocks, lds, st, P);
-    case 128: return launch_step_128(dm, events, mode, blocks, lds, st, P);
-    case 256: return launch_step_256(dm, events, mode, blocks, lds, st, P);
+    case 128: return launch_step_128(dm, events, mode, wv4, blocks, lds, st, P);
+    case 256: return launch_step_256(dm, events, mode, wv4, blocks, lds, st, P);
     default: return BRC_E_INVALID;
     }
 }
@@ -407,7 +408,7 @@ int brc_create(const brc_config* cfg, void** out) {
     e->cfg = c;
     e->npad = pick_npad(c.n);
     e->dm = pick_dm(c.delay_max);
-    e->rs = (c.n > 64) ? (uint32_t)TS : ring_steps(e->dm);
+    e->rs = ring_steps(e->dm);
     e->wide = e->npad > 64;
     e->ipw = e->wide ? 1 : 64 / e->npad;
     e->lpi = e->wide ? (uint32_t)e->npad : 64u;
@@ -428,9 +429,13 @@ int brc_create(const brc_config* cfg, void** out) {
     // wide exchange words per (key, type): connection peers send 8 count planes per link delay
     const uint32_t xw = c.peer_mode == BRC_PEER_CONNECTION ? 8u * nL : xwords_wide(c.delay_model, c.delay_max, e->dm);
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xw,
-                                            spec, c.key_window)
+                                            spec, c.key_window, e->rs)
                            : lds_bytes_per_wave(e->npad, e->NK, e->nkw, e->regmask ? 0u : nL, spec, c.key_window,
                                                 c.variants, e->rs, e->compact) * WPB;
+    // wide kernel at 4 waves per SIMD (128 VGPRs): DM <= 8 without delay-code planes in registers (constant /
+    // slow-set delays), sender peers, and LDS for four workgroups per CU
+    e->wide_wv4 = e->wide && e->dm <= 8 && !plane_model(c.delay_model) && c.peer_mode == BRC_PEER_SENDER &&
+                  e->lds_bytes <= 40u * 1024u;
     e->nval = value_ids(!e->compact && !e->wide);
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants, e->nval);
     // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8
@@ -811,8 +816,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
         e->life_done = true;
     } else {
         rc = e->regmask ? launch_step_64r(e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream, e->dparams)
-                        : launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, blocks, e->lds_bytes, e->stream,
-                                      e->dparams);
+                        : launch_step(e->npad, e->dm, c.event_capacity != 0, kmode, e->wide_wv4, blocks, e->lds_bytes,
+                                      e->stream, e->dparams);
     }
     if (rc == BRC_E_INVALID) { e->err = "no kernel instantiation"; return rc; }
     if (rc) { e->err = std::string("step kernel launch: ") + hipGetErrorString(hipGetLastError()); return rc; }

@@ -8,7 +8,7 @@
 
 namespace brc {
 
-constexpr int TS = 32;            // activity ring (steps); > max delay
+constexpr int TS = 32;            // activity ring (steps) at the largest DM; > max delay (ring_steps(dm) per kernel)
 #ifndef BRC_WPB
 #define BRC_WPB 1
 #endif
@@ -36,7 +36,7 @@ constexpr uint32_t GEN_FULL_CLEAR = 6000;   // host forces a full clear before t
 #endif
 constexpr int CHUNK_W = BRC_CHUNK_W;                // wide kernel: keys whose ballots are exchanged per barrier
 #ifndef BRC_WIDE_DCW
-#define BRC_WIDE_DCW 4
+#define BRC_WIDE_DCW 2     // 128 key-list positions per pass: keeps cfg5 at <= 40 KB (4 workgroups per CU)
 #endif
 // wide kernel: delivery-bitmap words per receiver = key-list positions per pass / 64
 __host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw < BRC_WIDE_DCW ? nkw : BRC_WIDE_DCW; }
@@ -171,7 +171,7 @@ __host__ __device__ inline uint32_t lds_bytes_per_wave(int npad, uint32_t NK, ui
 }
 
 // Bytes of dynamic LDS one workgroup of the wide kernel needs (brc_step_wide.h carve):
-// meta[NK] u64 | act[TS][nkw] u64 | dpos[DCW][NPAD] u64 | consensus area |
+// meta[NK] u64 | act[rs][nkw] u64 (rs = ring_steps(dm)) | dpos[DCW][NPAD] u64 | consensus area |
 // xb[2][CHUNK_W][nL][2][NW] u64 | outm[16][NW] u64 | sq[Q][NPAD] u8 | fresh[nkw] u64 | klist[NK] u16 |
 // red[12] u32 | pmw[2][CHUNK_W][NW] u32
 // consensus area: REFERENCE hm[4][NW][NPAD] u64;  SPEC cnt[Q][NPAD] u32 (one key variant per origin)
@@ -191,9 +191,10 @@ __host__ __device__ inline uint32_t xwords_wide(uint32_t model, uint32_t dmax, i
     return plane_model(model) ? (uint32_t)npl_of(dm) + 1u : delay_values(model, dmax);
 }
 
-__host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec, uint32_t Q) {
+__host__ __device__ inline uint32_t lds_bytes_wide(int npad, uint32_t NK, uint32_t nkw, uint32_t nL, bool spec, uint32_t Q,
+                                                    uint32_t rs) {
     const uint32_t nw = (uint32_t)npad / 64;
-    return 8 * (NK + TS * nkw + dpos_words_wide(nkw) * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
+    return 8 * (NK + rs * nkw + dpos_words_wide(nkw) * (uint32_t)npad + cons_words_wide(spec, (uint32_t)npad, Q) +
                 2 * CHUNK_W * nL * 2 * nw + 16 * nw) +
            Q * (uint32_t)npad + 8 * nkw + 2 * NK + 4 * (12 + 2 * CHUNK_W * nw);
 }
@@ -231,7 +232,8 @@ int launch_step_64(int dm, bool events, int mode, uint32_t blocks, uint32_t lds,
 // NPAD = 64 lean kernels with the (at most two) link-delay masks in registers (brc_kern_64r.hip)
 int launch_step_64r(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 // wide kernel (brc_step_wide.h): one workgroup of NPAD threads per instance
-int launch_step_128(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
-int launch_step_256(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+// wv4: the 4-waves-per-SIMD instantiation (wide_waves4: DM <= 8, no link-delay planes, sender peers)
+int launch_step_128(int dm, bool events, int mode, bool wv4, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
+int launch_step_256(int dm, bool events, int mode, bool wv4, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P);
 
 }  // namespace brc

@@ -57,8 +57,12 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return x;
 }
 
-template <int NPAD, int DM, bool EV, int MODE>
-__global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES)) void brc_step_wide(const Params* __restrict__ pp) {
+// WV: waves per SIMD the register allocation must allow (0: BRC_WIDE_WAVES / BRC_WIDE_WAVES16).  4 is
+// the instantiation for DM <= 8 under the constant / slow-set models (no delay-code planes in registers):
+// 128 VGPRs, and with the DM-sized ring and 2-word delivery bitmaps a cfg5 workgroup fits 40 KB of LDS, so
+// four workgroups share a CU (cfg5 const: 37.8 -> 31.9 ms, A/B round 5; uniform planes lose: 137.7 -> 139.8)
+template <int NPAD, int DM, bool EV, int MODE, int WV = 0>
+__global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES)) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     // u64 words per cell: CONN adds the lane's ECHO and READY send-count rings (Ring16, brc_step.h)
@@ -68,6 +72,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
     // saves (measured cfg5: geometric -20% kernel time, const/uniform +5%)
     constexpr bool SPARSE_D = DM > 8;
     constexpr int NW = NPAD / 64;
+    constexpr uint32_t TS = ring_steps(DM);              // activity-ring rows (> the largest delay)
     constexpr int NPL = npl_of(DM);                      // bit planes of a link's delay code
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
 
@@ -571,6 +576,14 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
         lane_rows = 0;
     }
 
+#ifdef BRC_STAMPS
+    // dev-only section timers (tools/stamps.py): per-wave s_memtime deltas, summed over the grid
+    uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+#define BRC_WSTAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
+#else
+#define BRC_WSTAMP(i) do {} while (0)
+#endif
     for (uint32_t it = 0; it < P.max_steps; ++it) {
         if (status != BRC_RUNNING) break;                 // workgroup-uniform
         const uint32_t rot = (t + 1) & (TS - 1);
@@ -616,6 +629,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
                 __syncthreads();
             }
         }
+        BRC_WSTAMP(0);
 
         // phase 1 of a chunk: ballot words "my ECHO / READY of key c was sent dly steps ago"
         // The key id, meta word and generation it reads stay in SGPRs for phase 2 (process): meta
@@ -780,6 +794,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
                     }
                 }
             }
+            BRC_WSTAMP(3);
             // SEND from the key's origin: arrives at t_send + delay(origin -> d)
             bool s_arr = false;
             const uint32_t dt = t - m_tsend(m);
@@ -841,6 +856,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
                 }
                 if (dl) log_ev(BRC_EV_DELIVER, d, 0, kp, s, m_value(m));
             }
+            BRC_WSTAMP(6);
             // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
             const uint64_t sb = __ballot(es || rs);
             if (sb) {
@@ -873,14 +889,18 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
                     const uint32_t buf = (p / CHUNK_W) & 1;
                     uint64_t mA[CHUNK_W];
                     ballots(p, buf, wA, kA, mA);
+                    BRC_WSTAMP(1);
                     __syncthreads();
+                    BRC_WSTAMP(2);
                     uint64_t wB[CHUNK_W];
                     uint32_t kB[CHUNK_W];
                     fetch(p + CHUNK_W, wB, kB);
+                    BRC_WSTAMP(2);
                     Unrolled<CHUNK_W>::run([&](auto ci) {
                         constexpr int c = decltype(ci)::value;
                         if (p + c < end) process(kA[c], wA[c], mA[c], buf, c, p + c - base);
                     });
+                    BRC_WSTAMP(7);
                     Unrolled<CHUNK_W>::run([&](auto ci) {
                         constexpr int c = decltype(ci)::value;
                         wA[c] = wB[c];
@@ -908,6 +928,7 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
                 }
             }
             __syncthreads();
+            BRC_WSTAMP(4);
         }
         flush_sends();
         clear_fresh();
@@ -928,8 +949,13 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
         else if (q_until <= t && inj_pos >= inj_cnt) status = BRC_QUIESCENT;
         if (d < nkw) s_act[row * nkw + d] = 0;
         any_rows &= ~(1u << row);
+        BRC_WSTAMP(5);
     }
     __syncthreads();
+#ifdef BRC_STAMPS
+    if (lane == 0) for (int i = 0; i < 8; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+#endif
+#undef BRC_WSTAMP
 
     // ---- write back
     for (uint32_t i = d; i < NK; i += NPAD) {
@@ -978,9 +1004,9 @@ __global__ __launch_bounds__(NPAD, (DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES
     }
 }
 
-template <int NPAD, int DMX, bool EV, int MODE>
+template <int NPAD, int DMX, bool EV, int MODE, int WV = 0>
 int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_step_wide<NPAD, DMX, EV, MODE>;
+    auto kern = brc_step_wide<NPAD, DMX, EV, MODE, WV>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;
@@ -989,7 +1015,18 @@ int launch_wide_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* 
 }
 
 template <int NPAD>
-int launch_step_wide(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+int launch_step_wide(int dm, bool events, int mode, bool wv4, uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
+    // the 4-wave instantiations (host-chosen, wide_waves4): same LDS carve, so the event-log runs take the 3-wave ones
+    if (wv4 && !events && dm <= 8 && mode != KMODE_CONN) {
+        if (dm == 4) {
+            if (mode == BRC_MODE_SPEC) return launch_wide_one<NPAD, 4, false, BRC_MODE_SPEC, 4>(blocks, lds, s, P);
+            if (mode == BRC_MODE_BEB) return launch_wide_one<NPAD, 4, false, BRC_MODE_BEB, 4>(blocks, lds, s, P);
+            return launch_wide_one<NPAD, 4, false, BRC_MODE_REFERENCE, 4>(blocks, lds, s, P);
+        }
+        if (mode == BRC_MODE_SPEC) return launch_wide_one<NPAD, 8, false, BRC_MODE_SPEC, 4>(blocks, lds, s, P);
+        if (mode == BRC_MODE_BEB) return launch_wide_one<NPAD, 8, false, BRC_MODE_BEB, 4>(blocks, lds, s, P);
+        return launch_wide_one<NPAD, 8, false, BRC_MODE_REFERENCE, 4>(blocks, lds, s, P);
+    }
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
         if (mode == BRC_MODE_SPEC) return events ? launch_wide_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_wide_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \

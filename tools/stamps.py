@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Dev-only: per-section cycle split of the narrow step kernel.
+"""Dev-only: per-section cycle split of the narrow (or, n > 128, the wide) step kernel.
 Needs a variant built with -DBRC_STAMPS (tools/variant.py stamps -DBRC_STAMPS); run with
 BRC_LIB=exp/stamps/libbrc_hip.so python tools/stamps.py [instances] [reference|spec|<configs.py workload>]."""
 import ctypes
@@ -24,17 +24,19 @@ else:
     eng = Engine(instances=inst, **kw)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
 out = (ctypes.c_ulonglong * 12)()
-dbg = lib.brc_dbg_stamps16 if eng.n <= 16 else lib.brc_dbg_stamps    # each unit keeps its own timers
+dbg = lib.brc_dbg_stamps16 if eng.n <= 16 else lib.brc_dbg_stamps256 if eng.n > 128 else lib.brc_dbg_stamps   # per unit
 eng.reset(); eng.run()
 dbg(out)
 eng.reset(); eng.run()
 dbg(out)
 tot = sum(out[:8])
-names = ["step head + key list", "key loop (BRB cells)", "consensus words", "actions", "stop checks",
+wide = eng.n > 128
+names = ["step head + key list", "ballots", "barrier + next fetch", "arrival counts", "pass end + consensus",
+         "sends, actions, stop", "cell update + store", "ring marks / t_quiet"] if wide else ["step head + key list", "key loop (BRB cells)", "consensus words", "actions", "stop checks",
          "consensus snapshot", "consensus row clears", "key-loop tail (ring rows)"]
 for nm, v in zip(names, out[:8]):
     print("%-24s %6.1f %%  (%.3g ticks)" % (nm, 100.0 * v / tot, v))
 kn = ["key-steps processed", "  no arrivals", "  only delivered cells", "  updated"]
-for nm, v in zip(kn, out[8:]):
+for nm, v in zip(kn if not wide else [], out[8:]):
     print("%-24s %.4g  (%.1f %%)" % (nm, v, 100.0 * v / max(1, out[8])))
 print("kernel ms %.2f" % eng.last_kernel_ms())

@@ -695,13 +695,20 @@ __global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_
                 }
             });
         };
+        // the chunk's key ids in one LDS read per 4 (p is a multiple of CHUNK_W, the list 8-B aligned and
+        // NK a multiple of 64, so the read stays inside it), then their cell words
+        static_assert(CHUNK_W % 4 == 0, "key ids are read 4 at a time");
         auto fetch = [&](uint32_t p, uint64_t (&ww)[CHUNK_W], uint32_t (&kk)[CHUNK_W]) {
+            uint64_t ids[CHUNK_W / 4];
+#pragma unroll
+            for (int g4 = 0; g4 < CHUNK_W / 4; ++g4)
+                ids[g4] = p + 4 * g4 < nkeys ? uni64(*(const uint64_t*)(s_klist + p + 4 * g4)) : 0ull;
             Unrolled<CHUNK_W>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 ww[c] = TIMES_NEVER;
                 kk[c] = 0;
                 if (p + c < nkeys) {
-                    kk[c] = uni32(s_klist[p + c]);
+                    kk[c] = (uint32_t)(ids[c / 4] >> (16 * (c % 4))) & 0xFFFFu;
                     ww[c] = mycells[(size_t)kk[c] * (CW * NPAD)];
                 }
             });
@@ -860,11 +867,9 @@ __global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_
             // sends of this wave: ring marks at t + every delay its sending lanes have; t_quiet
             const uint64_t sb = __ballot(es || rs);
             if (sb) {
-                uint32_t os = 0;
-                for (uint32_t ds = dset; ds; ds &= ds - 1) {
-                    const uint32_t i = (uint32_t)__ffs(ds) - 1;
-                    if (sb & s_outm[i * NW + wid]) os |= 1u << i;
-                }
+                // the delays some sending lane of this wave has to an honest receiver: a DPP OR of the
+                // senders' outsets (no LDS round trip per delay)
+                const uint32_t os = wave_or_all((es || rs) ? outset : 0u);
                 for (uint32_t x = os; x; x &= x - 1) {
                     const uint32_t r = (t + (uint32_t)__ffs(x)) & (TS - 1);
                     if (lane == 0) atomicOr((unsigned long long*)&s_act[r * nkw + (k >> 6)], 1ull << (k & 63));

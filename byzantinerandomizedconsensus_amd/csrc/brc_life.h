@@ -696,8 +696,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                                                                                 : 0x0101010101010101ull;
                             for (uint32_t q = 0; q < Q; ++q) {
                                 const uint64_t bq = b & (g0 << q);
-                                if (bq) s_cnt[q * 64 + lane] += (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
-                                                                 ((uint32_t)__popcll(bq & v2) << 20);
+                                if (bq) atomicAdd(&s_cnt[q * 64 + lane], (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
+                                                                 ((uint32_t)__popcll(bq & v2) << 20));
                             }
                             bits = 0;
                         }

@@ -1861,16 +1861,9 @@ void brc_step(const Params* __restrict__ pp) {
                         cons_deliver(bk);
                     }
                 }
-            } else
-#pragma unroll 1
-            for (uint32_t w = 0; w < nkw; ++w) {
-                uint64_t bits;
-                if constexpr (DBG) {
-                    bits = ((dwm >> w) & 1u) ? gdbits[w * 64] : 0ull;   // words written this step only
-                } else {
-                    bits = s_dbits[w * 64 + lane];
-                    s_dbits[w * 64 + lane] = 0;
-                }
+            } else {
+            // the deliveries of key word w (bits: this lane's), in slot order
+            auto cons_word = [&](const uint32_t w, uint64_t bits) {
                 if (!cons) bits = 0;
                 if constexpr (LEAN && SPEC) {
                     // SPEC (one key variant per origin): when every lane with deliveries in this word is
@@ -1905,8 +1898,8 @@ void brc_step(const Params* __restrict__ pp) {
                                                                                     : 0x0101010101010101ull;
                                 for (uint32_t q = 0; q < Q; ++q) {
                                     const uint64_t bq = b & (g0 << q);
-                                    if (bq) s_cnt[q * 64 + lane] += (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
-                                                                     ((uint32_t)__popcll(bq & v2) << 20);
+                                    if (bq) atomicAdd(&s_cnt[q * 64 + lane], (uint32_t)__popcll(bq) + ((uint32_t)__popcll(bq & v1) << 10) +
+                                                                     ((uint32_t)__popcll(bq & v2) << 20));
                                 }
                                 bits = 0;
                             }
@@ -1992,6 +1985,43 @@ void brc_step(const Params* __restrict__ pp) {
                     if constexpr (SPEC) spec_deliver(w * 64 + best);
                     else cons_deliver(w * 64 + best);
                 }
+            };
+            if constexpr (DBG) {
+                // HBM delivery words (lean SPEC): only the words written this step, their loads issued
+                // together (up to 8 at a time) instead of one round trip per word before its pass
+                uint32_t wm = dwm;                                  // uniform: the word passes ballot over slots (lanes)
+#pragma unroll 1
+                while (wm) {
+                    uint64_t bv[8];
+                    uint64_t wv = 0;                                // word ids, 5 bits each (nkw <= 32)
+                    uint32_t nw = 0;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        bv[i] = 0;
+                        if (wm) {
+                            const uint32_t w = (uint32_t)__ffs(wm) - 1u;
+                            wm &= wm - 1u;
+                            bv[i] = gdbits[w * 64];
+                            wv |= (uint64_t)w << (5 * i);
+                            ++nw;
+                        }
+                    }
+#pragma unroll 1
+                    for (uint32_t i = 0; i < nw; ++i) {
+                        uint64_t b = bv[0];
+#pragma unroll
+                        for (int j = 1; j < 8; ++j) b = i == (uint32_t)j ? bv[j] : b;
+                        cons_word((uint32_t)(wv >> (5 * i)) & 31u, b);
+                    }
+                }
+            } else {
+#pragma unroll 1
+                for (uint32_t w = 0; w < nkw; ++w) {
+                    const uint64_t bits = s_dbits[w * 64 + lane];
+                    s_dbits[w * 64 + lane] = 0;
+                    cons_word(w, bits);
+                }
+            }
             }
         }
         BRC_STAMP(2);

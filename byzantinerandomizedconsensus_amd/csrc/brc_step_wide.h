@@ -636,12 +636,17 @@ __global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_
         // changes in between only in t_quiet, through process's own atomicMax, which keeps the max.
         auto ballots = [&](uint32_t p, uint32_t buf, const uint64_t (&ww)[CHUNK_W], const uint32_t (&kk)[CHUNK_W],
                            uint64_t (&mm)[CHUNK_W]) {
+            // the chunk's metadata words first, all in flight together (the ballot-word writes below
+            // would otherwise order each key's read behind the previous key's writes)
+            Unrolled<CHUNK_W>::run([&](auto ci) {
+                constexpr int c = decltype(ci)::value;
+                mm[c] = p + c < nkeys ? uni64(s_meta[kk[c]]) : 0ull;
+            });
             Unrolled<CHUNK_W>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
                 if (p + c < nkeys) {
                     const uint32_t k = kk[c];
-                    const uint64_t m = uni64(s_meta[k]);
-                    mm[c] = m;
+                    const uint64_t m = mm[c];
                     const bool cur = m_s1(m) != 0 && real;
                     const uint64_t word = cur ? ww[c] : TIMES_NEVER;
                     const uint32_t dE = t - ((uint32_t)(word >> 32) & 0xFFFF), dR = t - (uint32_t)(word >> 48);
@@ -849,7 +854,7 @@ __global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_
             st_cells += has ? 1u : 0u;
             st_msgs += ((es ? 1u : 0u) + (CONN ? n_ready : (rs ? 1u : 0u))) * n;
             st_del += dl ? 1u : 0u;
-            if (dl) s_dpos[(pos >> 6) * NPAD + d] |= 1ull << (pos & 63);   // pos: in this pass
+            if (dl) atomicOr((unsigned long long*)&s_dpos[(pos >> 6) * NPAD + d], 1ull << (pos & 63));   // pos: in this pass (no-return LDS OR)
             if (EV) {
                 const uint32_t kp = (k >> qsh), s = m_s1(m) - 1u;
                 if (es) log_ev(had_es ? BRC_EV_COPY : BRC_EV_SEND, d, BRC_ECHO, kp, s, m_value(m));

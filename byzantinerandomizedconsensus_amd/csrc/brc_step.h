@@ -942,6 +942,51 @@ void brc_step(const Params* __restrict__ pp) {
         }
     };
 
+    // a SEND / KEY record of this lane's instance (the caller's `mine`): the slot's metadata (lane d = 0),
+    // and for a SEND its destinations, ring marks at the delays in os and its message count.  Returns
+    // whether the slot was (re)allocated (lean: a fresh row)
+    auto send_rec = [&](const InjDev& r, const uint32_t os) -> bool {
+        const bool is_send = r.kind == BRC_INJ_SEND;
+        const uint32_t k = r.slot;
+        bool fresh = false;
+        if (d == 0) {
+            uint64_t m = s_meta[mbase + k];
+            uint32_t gen = LEAN ? 0u : s_gen[mbase + k] & GEN_MASK;
+            const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
+            if ((!declared && m_s1(m) != 0 && (t < m_tquiet(m) || (LEAN && ring_busy(k)))) || r.s >= P.s_limit) {
+                ovf = true;
+            } else {
+                uint32_t tq = m_tquiet(m);
+                // a declared key holds its slot at least until the next step
+                if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; fresh = true; }
+                if (is_send) tq = max(tq, t + hibit(os));
+                m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
+                s_meta[mbase + k] = m;
+                const bool restricted = is_send && (r.dst & all64) != all64;
+                if (!LEAN) s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
+                if (LEAN && restricted) s_meta[mbase + k] = m | M_RESTRICTED;
+                st_smax = max(st_smax, (uint32_t)r.s);
+                if (is_send) {
+                    gp(P.kdst)[inst * NK + k] = r.dst;
+                    mark_lane(k, os, BRC_SEND);
+                    st_msgs += __popcll(r.dst & all64);
+                    log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
+                }
+            }
+        }
+        return fresh;
+    };
+    // the delays at which this lane (an honest destination of SEND r) hears the SEND's origin
+    auto send_delay_set = [&](const InjDev& r, const bool mine) -> uint32_t {
+        uint32_t myset = 0;
+        if (r.kind == BRC_INJ_SEND && mine && honest && ((r.dst >> d) & 1ull)) {
+            uint32_t j = 0;
+            for (uint32_t ds = dset; ds; ds &= ds - 1, ++j)
+                if ((Lmask(j) >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
+        }
+        return myset;
+    };
+
     // ---- actions stamped t (performed after step t's messages)
     auto do_actions = [&]() -> bool {
         bool mine_any = false;
@@ -972,17 +1017,41 @@ void brc_step(const Params* __restrict__ pp) {
                 if constexpr (!SPEC) {
                     if (mine && honest && d == r.node) cons_deliver_vh((uint32_t)r.value & VMASK, r.slot);
                 }
+            } else if (!LEAN && IPW > 1 && (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) && !(r.type & 2u)) {
+                // a run of SEND / KEY records at this step (within the staged window, no extra SEND):
+                // the item's instances are independent, so every segment applies its own records, in
+                // order, all segments at once (cfg3's equivocation pattern: 40 such records per wave)
+                const uint32_t p0 = inj_pos - 1;
+                uint32_t p1 = inj_pos;
+                while (p1 < inj_cnt && p1 - injc_base < INJ_CACHE) {
+                    const InjDev q = inj_at(p1);
+                    if (q.t != t || (q.kind != BRC_INJ_SEND && q.kind != BRC_INJ_KEY) || (q.type & 2u)) break;
+                    ++p1;
+                }
+                inj_pos = p1;
+                uint32_t myrecs = 0;
+                for (uint32_t p = p0; p < p1; ++p)
+                    if (seg == (int)inj_at(p).seg) myrecs |= 1u << (p - p0);
+                while (__any(myrecs != 0)) {
+                    InjDev q = r;
+                    const bool has = myrecs != 0;
+                    if (has) {
+                        const uint32_t i = (uint32_t)__ffs(myrecs) - 1u;
+                        myrecs &= myrecs - 1;
+                        q = inj_at(p0 + i);              // inside the staged window: no refill
+                    }
+                    const bool mq = has && running;
+                    mine_any |= mq;
+                    const uint32_t os = seg_or<NPAD, uint32_t>(send_delay_set(q, mq));
+                    if (mq) {
+                        send_rec(q, os);
+                        q_until = max(q_until, t + hibit(os));
+                    }
+                }
             } else if (r.kind == BRC_INJ_SEND || r.kind == BRC_INJ_KEY) {
                 // KEY declares a (Byzantine) key without sending; SEND sends it, allocating the
                 // slot first unless that key was declared and not yet sent
-                const bool is_send = r.kind == BRC_INJ_SEND;
-                uint32_t myset = 0;
-                if (is_send && mine && honest && ((r.dst >> d) & 1ull)) {
-                    uint32_t j = 0;
-                    for (uint32_t ds = dset; ds; ds &= ds - 1, ++j)
-                        if ((Lmask(j) >> r.node) & 1) myset = 1u << (__ffs(ds) - 1);
-                }
-                const uint32_t os = wave_or(myset);
+                const uint32_t os = wave_or(send_delay_set(r, mine));
                 // a SEND of a key already SENT (another origin or again, one payload): brc_inject has
                 // put it in the item's extra-SEND records (r.type bit 1; bit 0: a repeat of this node's)
                 if (!LEAN && (r.type & 2u)) {
@@ -1003,35 +1072,9 @@ void brc_step(const Params* __restrict__ pp) {
                     }
                     if (mine) q_until = max(q_until, t + hibit(os));
                 } else if (mine) {
-                    const uint32_t k = r.slot;
-                    bool fresh = false;                  // lean: the slot is (re)allocated: fresh row
-                    if (d == 0) {
-                        uint64_t m = s_meta[mbase + k];
-                        uint32_t gen = LEAN ? 0u : s_gen[mbase + k] & GEN_MASK;
-                        const bool declared = m_s1(m) == r.s + 1u && m_tsend(m) == NEVER && is_send;
-                        if ((!declared && m_s1(m) != 0 && (t < m_tquiet(m) || (LEAN && ring_busy(k)))) || r.s >= P.s_limit) {
-                            ovf = true;
-                        } else {
-                            uint32_t tq = m_tquiet(m);
-                            // a declared key holds its slot at least until the next step
-                            if (!declared) { gen = (gen + 1) & GEN_MASK; tq = t + 1; fresh = true; }
-                            if (is_send) tq = max(tq, t + hibit(os));
-                            m = m_pack(r.s + 1, is_send ? t : NEVER, tq, r.node, (uint32_t)(uint8_t)r.value);
-                            s_meta[mbase + k] = m;
-                            const bool restricted = is_send && (r.dst & all64) != all64;
-                            if (!LEAN) s_gen[mbase + k] = (uint16_t)(gen | (restricted ? GEN16_RESTRICTED : 0u));
-                            if (LEAN && restricted) s_meta[mbase + k] = m | M_RESTRICTED;
-                            st_smax = max(st_smax, (uint32_t)r.s);
-                            if (is_send) {
-                                gp(P.kdst)[inst * NK + k] = r.dst;
-                                mark_lane(k, os, BRC_SEND);
-                                st_msgs += __popcll(r.dst & all64);
-                                log_ev(BRC_EV_SEND, r.node, BRC_SEND, (k >> qsh), r.s, (uint32_t)(uint8_t)r.value);
-                            }
-                        }
-                    }
+                    const bool fresh = send_rec(r, os);
                     if constexpr (LEAN) {
-                        if (__ballot(fresh)) cst(uni32(k), C32_FRESH);
+                        if (__ballot(fresh)) cst(uni32((uint32_t)r.slot), C32_FRESH);
                     }
                     q_until = max(q_until, t + hibit(os));
                 }

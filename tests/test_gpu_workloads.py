@@ -70,6 +70,31 @@ def test_restricted_sends_wide_vs_oracle(runner, n, f, model, dmax, peer_mode):
     assert any(r["events"]["deliver"] for r in got)
 
 
+@pytest.mark.parametrize("n,f,model,dmax", [(16, 3, 1, 4), (8, 2, 2, 3), (13, 2, 3, 8)])
+def test_record_runs_per_segment_vs_oracle(runner, n, f, model, dmax):
+    """Narrow kernels that pack several instances into one wave (n <= 16: 4 or 8 per item) apply a
+    step's run of SEND / KEY records per instance, all instances at once (brc_step.h do_actions).
+    Consecutive instances with different numbers of declared and (restricted) SENT Byzantine keys
+    at the same steps -- some none, some several -- each equal the oracle run alone."""
+    rng = random.Random(1000 + n)
+    byz = list(range(n - f, n))
+    specs = []
+    for g in range(12):
+        extra = []
+        for b in rng.sample(byz, rng.randint(0, len(byz))):
+            dst = sum(1 << d for d in range(n) if rng.random() < 0.7)
+            t = rng.randint(0, 1)
+            extra.append(dict(t=t, kind="byz_key", kp=b, s=0, value=0, payload="BYZ %d" % b))
+            if rng.random() < 0.8:
+                extra.append(dict(t=t, kind="byz", src=b, type=1, kp=b, s=0, dst=dst))
+        sends = [(rng.randint(0, 1), o, 0) for o in rng.sample(range(n - f), 2)]
+        sp = S.brb_spec(n, f, 0xA11 + n, model, dmax, 700 + g, sends, byzantine=byz, extra=extra)
+        sp["name"] = "records%d/%d" % (n, g)
+        specs.append(sp)
+    got = _compare(runner, specs)
+    assert any(r["events"]["deliver"] for r in got)
+
+
 @pytest.mark.parametrize("n,f,model,dmax", [(100, 33, 1, 4), (128, 42, 2, 8)])
 def test_equivocation_wide_vs_oracle(runner, n, f, model, dmax):
     """SURVEY §8(d) cfg3's equivocation on a large committee: every Byzantine replica SENDs "0"

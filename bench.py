@@ -286,8 +286,22 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
         "kernel": kernel,
         "workload": workload_name(mode, cap, per),
         "round_cap": cap,
+        "parity": parity_basis(mode),
     }
     return leg
+
+
+def parity_basis(leg):
+    """What the leg's results are pinned to: the reference protocol's legs to the reference
+    itself (reference-harness fixtures + the C oracle pinned by them); SPEC to the oracle's restatement
+    of the intended protocol only -- the reference's coin branch (core/byzantinerandomizedconsensus.py:
+    89-92) is unreachable, so no reference run can produce a SPEC vector."""
+    if LEGS[leg][0] == "spec":
+        return ("C-oracle restatement of the intended protocol only (the reference's coin branch, "
+                "core/byzantinerandomizedconsensus.py:89-92, is dead code): parity pinned by the restatement, "
+                "not by reference fixtures")
+    return ("reference-harness fixtures (tests/golden, the unmodified reference classes) and the C oracle they "
+            "pin; 2^20 batch oracle-sampled in tests/test_gpu_fullsize.py")
 
 
 def workload_name(leg, cap, per):
@@ -349,7 +363,7 @@ def main():
             "collective": (dist.get_backend() + " all-reduce of the statistics") if dist is not None else None,
         }
         for k in ("kernel", "kernel_ms", "decided_fraction", "decide_round_hist", "decided_value_hist",
-                  "agreement_violations", "replica_message_steps_per_s", "counts", "roofline"):
+                  "agreement_violations", "replica_message_steps_per_s", "counts", "roofline", "parity"):
             out[k] = head[k]
         for mode, leg in legs.items():
             if mode != head_mode:

@@ -124,6 +124,18 @@ def measured_profile(name, kernel_ms):
     return best
 
 
+def parity_basis(mode, L):
+    """What a workload's results are pinned to.  SPEC and BEB rest on the C oracle's
+    restatement alone: the reference's coin branch (core/byzantinerandomizedconsensus.py:89-92) is
+    unreachable and its BEBroadcast.__init__ raises (core/bebroadcast.py), so no reference run can
+    produce their vectors."""
+    if mode == L.MODE_SPEC:
+        return "C-oracle restatement of the intended protocol only (reference coin branch :89-92 is dead code)"
+    if mode == L.MODE_BEB:
+        return "C-oracle restatement only (the reference's BEBroadcast cannot be constructed)"
+    return "reference-harness fixtures (tests/golden) and the C oracle they pin"
+
+
 def attach_profile(out, name, kernel_ms):
     prof = measured_profile(name, kernel_ms)
     if prof:
@@ -236,6 +248,7 @@ def main():
                 "kernel": kname,
                 "roofline": roofline(name, n, bpc, st["cell_steps"] / world, kernel_ms, kw.get("peer_mode", 0),
                                      kernel=kname),
+                "parity": parity_basis(kw.get("mode", L.MODE_REFERENCE), L),
             }), flush=True)
     if dist is not None:
         dist.destroy_process_group()

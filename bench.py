@@ -239,14 +239,21 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     traffic = prof.get("hbm_bytes_per_launch") if prof else None
     if kernel == "life":
         # the key-lifetime kernel (csrc/brc_life.h) keeps a key's cells in registers for its whole
-        # lifetime: no cell bytes move, HBM carries only the per-instance results
-        roof = {"bound": "issue", "kernel": "brc_life", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": None, "traffic": traffic,
+        # lifetime: no cell bytes move, HBM carries only the per-instance results.  Its roof is
+        # instruction issue: frac = the busier of the two issue ports, from the same-build PMC
+        iss = prof.get("issue") if prof else None
+        frac = max(iss["valu_busy"], iss["salu_per_cu_cycle"]) if iss else None
+        roof = {"bound": "issue", "kernel": "brc_life", "achieved": frac, "peak": 1.0,
+                "unit": "issue-port fraction", "frac": frac, "traffic": traffic,
                 "traffic_frac": (traffic / secs / 1e9 / HBM_PEAK_GBS) if traffic else None,
                 "survey_model_gbs": SURVEY_BYTES_PER_CELL_STEP * cs_gpu / secs / 1e9,
                 "cell_steps_per_s": cs_gpu / secs, "cell_bytes": 0, "units_per_launch": cs_gpu / launches,
-                "note": "no HBM cell traffic (cells stay in registers for a key's lifetime): bound by instruction "
-                        "issue, not HBM; survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step (bytes this "
+                "note": "no HBM cell traffic (cells stay in registers for a key's lifetime), so the roof is "
+                        "instruction issue: frac = max(VALU busy, SALU per CU-cycle) of the same-build rocprofv3 "
+                        "PMC (roofline.profile.source): VALU busy = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x "
+                        "cycles), SALU = SQ_INSTS_SALU / (256 CUs x cycles), cycles = GRBM_GUI_ACTIVE / 8 "
+                        "(profiles/summarize.py issue_block); null when no profile of this build agrees with the "
+                        "live kernel time; survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step (bytes this "
                         "kernel never moves)" % SURVEY_BYTES_PER_CELL_STEP}
     else:
         # algorithmic bytes of THIS layout: the 4-B cell word read + written per cell-step
@@ -306,12 +313,18 @@ def parity_basis(leg):
 
 def workload_name(leg, cap, per):
     proto, peer, model, dmax, window = LEGS[leg]
-    return "cfg4: n=64 f=21 %s consensus to %s, %s, %s peers, key window %d, %d instances/GPU" % (
+    form = ""
+    if peer == "connection":
+        # the key-lifetime kernel's two forms (csrc/brc_life.h): under slow-set delays the receivers of one
+        # class see the same arrivals, so it counts them once per class -- exact for that model only
+        form = (", two-class arrival counts (slow-set symmetry: counted once per receiver class)" if model == "slowset"
+                else ", per-link arrival counts (the general form)")
+    return "cfg4: n=64 f=21 %s consensus to %s, %s, %s peers%s, key window %d, %d instances/GPU" % (
         "SPEC-protocol (common coin)" if proto == "spec" else "reference-protocol",
         "first decision" if cap == 1 else "%d decisions" % cap,
         "slow-set delays D=%d" % dmax if model == "slowset" else "per-link uniform[1,%d] delays" % dmax,
         "connection-identity (core/brbroadcast.py:69)" if peer == "connection" else "sender-identity",
-        window, per)
+        form, window, per)
 
 
 def main():

@@ -176,6 +176,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 template <typename T> using gptr_t = __attribute__((address_space(1))) T*;
 template <typename T> __device__ __forceinline__ gptr_t<T> gp(T* p) { return (gptr_t<T>)p; }
 
+
 // one 24-B injection record through global (not flat) loads
 // the first 24 B of a record (everything but dst_hi, which only the wide kernel reads)
 __device__ __forceinline__ InjDev load_inj(const InjDev* p) {
@@ -361,6 +362,9 @@ __device__ __forceinline__ Ring16 ring_put(Ring16 r, uint32_t tl, uint32_t t, ui
 #endif
 #ifndef BRC_DACC
 #define BRC_DACC 1           // lean REFERENCE: deliveries collected per key word in a register (0: LDS atomics)
+#endif
+#ifndef BRC_OOBST
+#define BRC_OOBST 1          // lean kernels: the key loop's cell stores unconditional, kept words dropped out of range
 #endif
 #ifndef BRC_PK
 #define BRC_PK 1             // lean kernels: a key pair's cell updates in the two 16-bit halves of a register
@@ -632,6 +636,14 @@ void brc_step(const Params* __restrict__ pp) {
     const uint32_t lv4 = (uint32_t)lane * 4u;
     auto cld = [&](uint32_t k) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(crs, lv4, k * 256u, 0); };
     auto cst = [&](uint32_t k, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, crs, lv4, k * 256u, 0); };
+    // the key loop's cell store as ONE unconditional instruction: lanes that keep their word get a
+    // voffset past the resource's range, whose stores the buffer unit drops.  A store skipped by an
+    // exec branch instead leaves the compiler unsure how many vector-memory ops are outstanding, and
+    // its vmcnt waits then assume the fewest -- each pair waited for more cell loads than it reads
+    auto cst_if = [&](uint32_t k, uint32_t v, bool wr) {
+        if constexpr (BRC_OOBST) __builtin_amdgcn_raw_buffer_store_b32(v, crs, wr ? lv4 : 0x80000000u, k * 256u, 0);
+        else if (wr) cst(k, v);
+    };
     // lean: this lane's own key slots (bit s mod Q) allocated since the last flush; the wave
     // rewrites those rows fresh (flush_clears) before anything reads them
     uint32_t clr = 0;
@@ -1741,6 +1753,12 @@ void brc_step(const Params* __restrict__ pp) {
             // the compiler's wait for slot 0 would then drain every load)
             Unrolled<LC>::run([&](auto ci) {
                 constexpr int c = decltype(ci)::value;
+                // OOBST: the loop's order (two stores, then two loads, per pair) from the start, with
+                // stores that write nothing, so the loop entry's count of outstanding ops is the loop's own
+                if constexpr (BRC_OOBST && (c % 2 == 0)) {
+                    __builtin_amdgcn_raw_buffer_store_b32(0u, crs, 0x80000000u, 0u, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(0u, crs, 0x80000000u, 256u, 0);
+                }
                 kk[c] = kid(c);
                 w[c] = cell(kk[c]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -1779,11 +1797,19 @@ void brc_step(const Params* __restrict__ pp) {
                     uint32_t mk_a = NOKEY;
                     uint64_t mk_v = 0;
                     if (p + c < nkeys) process_pair(ent, mp, lo, nw, wr, mk_a, mk_v);
-                    if (wr[0]) cst(kk[c] & TB_KEY, nw[0]);
-                    if (wr[1]) cst(kk[c + 1] & TB_KEY, nw[1]);
+                    cst_if(kk[c] & TB_KEY, nw[0], wr[0]);
+                    cst_if(kk[c + 1] & TB_KEY, nw[1], wr[1]);
                     // refill (none after the last chunk: no load is left in flight past the loop, so the
                     // code after it neither waits for one nor keeps its registers)
-                    if (p + LC < nkeys) {
+                    if constexpr (BRC_OOBST) {
+                        // unconditional too (a skipped load is the same uncertainty as a skipped store):
+                        // after the last chunk the loads fall out of range, return 0 and touch no memory
+                        const uint32_t rv = (p + LC < nkeys) ? lv4 : 0x80000000u;
+                        kk[c] = uni32((uint32_t)knext[c / 2]);
+                        w[c] = __builtin_amdgcn_raw_buffer_load_b32(crs, rv, (kk[c] & TB_KEY) * 256u, 0);
+                        kk[c + 1] = uni32((uint32_t)(knext[c / 2] >> 32));
+                        w[c + 1] = __builtin_amdgcn_raw_buffer_load_b32(crs, rv, (kk[c + 1] & TB_KEY) * 256u, 0);
+                    } else if (p + LC < nkeys) {
                         kk[c] = uni32((uint32_t)knext[c / 2]);
                         w[c] = cell(kk[c]);
                         kk[c + 1] = uni32((uint32_t)(knext[c / 2] >> 32));

@@ -44,12 +44,17 @@ FLOOR_BYTES_PER_CELL_STEP = 2 * CELL_BYTES                      # this layout: t
 HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROARCH.md
 SPEC_TILE = 1 << 20                                             # SPEC (Q = 8) instances per engine tile
 MANY_CAP = 8                                                    # the many leg's round cap
+LONG_CAP = 64                                                   # SURVEY cfg4's round cap (long, spec64 legs)
 # leg -> (protocol mode, peer mode, delay model, delay max, key window)
 LEGS = {"reference": ("reference", "sender", "slowset", DELAY_MAX, 4),
         "spec": ("spec", "sender", "slowset", DELAY_MAX, 8),
         "conn": ("reference", "connection", "slowset", DELAY_MAX, 4),
         "connu": ("reference", "connection", "uniform", 2, 4),
-        "many": ("reference", "sender", "slowset", DELAY_MAX, 32)}
+        "many": ("reference", "sender", "slowset", DELAY_MAX, 32),
+        "long": ("reference", "sender", "slowset", DELAY_MAX, 128),
+        "spec64": ("spec", "sender", "slowset", DELAY_MAX, 8)}
+# legs with a round cap of their own (the others take --round-cap)
+LEG_CAP = {"many": MANY_CAP, "long": LONG_CAP, "spec64": LONG_CAP}
 
 
 def parse():
@@ -177,9 +182,9 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
     from byzantinerandomizedconsensus_amd import shard
     per = args.instances
     first, count = shard.shard_range(per * world, world, rank)     # global instance ids of this rank
-    tile = min(count, SPEC_TILE) if mode == "spec" else count
+    tile = min(count, SPEC_TILE) if LEGS[mode][0] == "spec" else count
     tiles = [(first + o, min(tile, count - o)) for o in range(0, count, tile)]
-    cap = args.many_cap if mode == "many" else args.round_cap
+    cap = args.many_cap if mode == "many" else LEG_CAP.get(mode, args.round_cap)
     eng = make_engine(mode, tiles[0][1], tiles[0][0], local, cap)
 
     def barrier():

@@ -45,6 +45,7 @@ class EngineError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("%s (%d): %s" % (ERRORS.get(code, "error"), code, msg))
         self.code = code
+        self.code = code
 
 
 class Config(ctypes.Structure):

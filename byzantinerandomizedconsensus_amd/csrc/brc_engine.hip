@@ -169,6 +169,7 @@ struct Engine {
     unsigned long long* gcount = nullptr;
     uint64_t* dbits = nullptr;                   // lean SPEC: per-wave delivery bitmaps (brc_step.h DBG)
     uint64_t* dring = nullptr;                   // per-link lifetime kernel: delivery bitmap ring (brc_life.h)
+    uint32_t* lmeta = nullptr;                   // lifetime kernel, key windows >= 64: slot metadata in HBM
     uint64_t* xsend = nullptr; uint32_t* xsn = nullptr;   // extra-SEND records (non-lean step kernels)
     bool life_pl = false;                        // lifetime kernel in its per-link delay form
     uint32_t life_rw = LIFE_RW;                  // ... its delivery-ring rows (LIFE_RW16 for delays above 8)
@@ -239,7 +240,7 @@ static int launch_step(int npad, int dm, bool events, int mode, bool wv4, uint32
 static void free_all(Engine* e) {
     void* ps[] = {e->cells, e->meta, e->mgen, e->kdst, e->act, e->actany, e->items, e->inst, e->istats,
                   e->cons0, e->cons1, e->hmask, e->inj, e->inj_off, e->inj_cnt, e->byz, e->prop, e->events,
-                  e->event_count, e->gcount, e->dbits, e->dring, e->xsend, e->xsn, e->dparams};
+                  e->event_count, e->gcount, e->dbits, e->dring, e->lmeta, e->xsend, e->xsn, e->dparams};
     for (void* p : ps) if (p) (void)hipFree(p);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -460,9 +461,15 @@ int brc_create(const brc_config* cfg, void** out) {
                               !(e->life_pl && c.key_window * c.variants > 32);
         bool big = e->compact && c.key_window * c.variants > 32;          // the lean kernels take <= 32
         if (!big && e->compact && c.peer_mode == BRC_PEER_SENDER && hipSetDevice(c.device) == hipSuccess) {
+            // the step kernel's whole per-instance state (cells, slot metadata / generations / destinations,
+            // activity ring) against 90 % of the device's TOTAL memory: the choice depends on the
+            // configuration and the device model only, never on what else holds memory at the time (an
+            // engine whose state fits but cannot be allocated now fails brc_create with BRC_E_NOMEM)
             size_t fr = 0, tot = 0;
-            const size_t cells = (size_t)e->nitems * (e->NK + 1) * 64 * 4;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && cells > fr / 10 * 9) big = true;
+            const size_t keys = (size_t)c.instances * e->NK;
+            const size_t need = (size_t)e->nitems * (e->NK + 1) * 64 * 4 + keys * (8 + 4 + 8) +
+                                (size_t)e->nitems * e->rs * e->nkw * act_types(true, 1) * 8;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && need > tot / 10 * 9) big = true;
             (void)hipGetLastError();
         }
         e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION || big);
@@ -505,6 +512,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec && e->step_ok) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
         {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * e->life_rw * e->nkw * 64 * 8 : 8},
+        {(void**)&e->lmeta, (e->life_cfg && life_hbm_meta(c.key_window, e->life_pl)) ? (size_t)e->nitems * e->NK * 4 : 8},
         // extra-SEND records: the non-lean narrow kernels only (the lean and wide kernels refuse extra SENDs)
         {(void**)&e->xsend, (e->compact || e->wide) ? 8 : (size_t)e->nitems * XSEND_MAX * 24},
         {(void**)&e->xsn, (e->compact || e->wide) ? 8 : (size_t)e->nitems * 4},
@@ -519,6 +527,7 @@ int brc_create(const brc_config* cfg, void** out) {
         if (hipMalloc(&e->event_count, 8) != hipSuccess) return fail(BRC_E_NOMEM);
     }
     e->cells_ready = !e->life_cfg;
+    e->last_life = e->life_cfg;       // brc_last_kernel before the first run: the kernel a fresh run launches
     if (hipMemsetAsync(e->inj_off, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->inj_cnt, 0, (size_t)e->nitems * 4, e->stream) != hipSuccess) return fail(BRC_E_HIP);
     if (hipMemsetAsync(e->kdst, 0, keys * 8 * e->bw, e->stream) != hipSuccess) return fail(BRC_E_HIP);   // keys = 1: 8 B
@@ -581,6 +590,11 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
     if (!e || (!list && count)) return BRC_E_INVALID;
     if (e->pattern_active) { e->err = "explicit injections cannot be combined with byz_pattern"; return BRC_E_STATE; }
     const brc_config& c = e->cfg;
+    if (!e->step_ok && count) {
+        e->err = "this engine runs on the key-lifetime kernel only (its step-kernel state does not fit the device, "
+                 "or a key window above 32 at n in 33..64 with sender peers): no injections";
+        return BRC_E_UNSUPPORTED;
+    }
     const uint64_t all = (c.n >= 64) ? ~0ull : ((1ull << c.n) - 1);
     std::vector<ItemState> its;
     std::vector<InstState> ist;
@@ -801,7 +815,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     P.inst = e->inst; P.istats = e->istats; P.cons0 = e->cons0; P.cons1 = e->cons1; P.hmask = e->hmask;
     P.inj = e->inj; P.inj_off = e->inj_off; P.inj_cnt = e->inj_cnt; P.byz = e->byz; P.prop = e->prop;
     P.events = e->events; P.event_count = e->event_count; P.gcount = e->gcount; P.dbits = e->dbits;
-    P.dring = e->dring; P.xsend = e->xsend; P.xsn = e->xsn;
+    P.dring = e->dring; P.lmeta = e->lmeta; P.xsend = e->xsend; P.xsn = e->xsn;
     const uint32_t blocks = e->wide ? (uint32_t)e->nitems : (uint32_t)((e->nitems + WPB - 1) / WPB);
     e->hparams = P;
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
@@ -811,7 +825,8 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     e->fresh = false;
     e->last_life = life;
     if (life) {
-        rc = launch_life(kmode, e->life_pl, e->life_rw == LIFE_RW16, c.key_window >= 64, (uint32_t)e->nitems,
+        rc = launch_life(kmode, e->life_pl, e->life_rw == LIFE_RW16, c.key_window >= 64,
+                         life_hbm_meta(c.key_window, e->life_pl), (uint32_t)e->nitems,
                          e->life_lds, e->stream, e->dparams);
         e->life_done = true;
     } else {

@@ -101,6 +101,7 @@ struct Params {
     brc_event* events; unsigned long long* event_count;
     uint64_t* dbits;              // lean SPEC: per-wave delivery bitmaps [item][nkw][64] (brc_step.h DBG)
     uint64_t* dring;              // per-link key-lifetime kernel: delivery bitmap ring [item][LIFE_RW or LIFE_RW16][nkw][64] (brc_life.h)
+    uint32_t* lmeta;              // key-lifetime kernel, key windows >= 64: key-slot metadata [item][NK] in HBM (brc_life.h)
     uint64_t* xsend;              // non-lean step kernels: extra-SEND records [item][XSEND_MAX][3] (brc_step.h)
     uint32_t* xsn;                // ... records in use per item
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
@@ -211,15 +212,24 @@ inline uint64_t cons_bytes_per_item(bool spec, bool wide, uint32_t lanes, uint32
 //   meta[NK] u32 | two-class form: dA[NK], dB[NK] u8 (each receiver class's delivery step of the key,
 //   0x80 | step mod 128) | (8-B aligned) consensus area (cons_words at NPAD = 64)
 constexpr uint32_t LIFE_RW = 32;
+// Key windows >= 32 in the two-class form (life_hbm_meta): the slot metadata lives in HBM (P.lmeta) and
+// LDS keeps only the class delivery steps plus a 128-word snapshot of the metadata of the key words a
+// consensus pass reads (their own instantiations, brc_life<..., HMT>).
+#ifndef BRC_LIFE_HM_Q
+#define BRC_LIFE_HM_Q 32
+#endif
+__host__ __device__ inline bool life_hbm_meta(uint32_t Q, bool perlink) { return !perlink && Q >= BRC_LIFE_HM_Q; }
 __host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, bool spec, uint32_t Q, uint32_t nv, bool perlink) {
-    return ((4 * NK + (perlink ? 0u : 2 * NK) + 7) & ~7u) + 8 * cons_words(spec, 8, Q, nv);
+    const uint32_t meta = life_hbm_meta(Q, perlink) ? 4u * 128u : 4u * NK;
+    return ((meta + (perlink ? 0u : 2 * NK) + 7) & ~7u) + 8 * cons_words(spec, 8, Q, nv);
 }
 // Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
 // (perlink: uniform / geometric delays, delivery bitmaps in P.dring; dm16: delays up to 16, whose
 // keys live up to 64 steps: P.dring has LIFE_RW16 rows)
 constexpr uint32_t LIFE_RW16 = 64;
 // qbig: key windows of 64 / 128 (two-class form, not SPEC)
-int launch_life(int mode, bool perlink, bool dm16, bool qbig, uint32_t blocks, uint32_t lds, hipStream_t s,
+// hm: the slot metadata in HBM (life_hbm_meta)
+int launch_life(int mode, bool perlink, bool dm16, bool qbig, bool hm, uint32_t blocks, uint32_t lds, hipStream_t s,
                 const Params* P);
 
 // Step-kernel launchers, one translation unit per replica-set width NPAD (brc_kern_<NPAD>.hip).

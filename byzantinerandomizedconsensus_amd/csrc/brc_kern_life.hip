@@ -14,9 +14,18 @@ static int launch_life_pl(int mode, uint32_t blocks, uint32_t lds, hipStream_t s
 }
 // perlink: uniform / geometric delays (per-receiver delay masks, HBM delivery bitmaps); dm16: delays up
 // to 16 (the per-link form's 64-row ring); qbig: key windows of 64 / 128 (two-class form, not SPEC)
-int launch_life(int mode, bool perlink, bool dm16, bool qbig, uint32_t blocks, uint32_t lds, hipStream_t s,
+int launch_life(int mode, bool perlink, bool dm16, bool qbig, bool hm, uint32_t blocks, uint32_t lds, hipStream_t s,
                 const Params* P) {
+    if (hm && !qbig) {
+        // key window 32, two-class form: the slot metadata in HBM (brc_internal.h life_hbm_meta)
+        if (perlink || mode == BRC_MODE_SPEC) return BRC_E_INVALID;
+        if (mode == BRC_MODE_BEB) return launch_life_one<BRC_MODE_BEB, false, 8, false, true>(blocks, lds, s, P);
+        if (mode == BRC_MODE_REFERENCE) return launch_life_one<BRC_MODE_REFERENCE, false, 8, false, true>(blocks, lds, s, P);
+        if (mode == KMODE_CONN) return launch_life_one<KMODE_CONN, false, 8, false, true>(blocks, lds, s, P);
+        return BRC_E_INVALID;
+    }
     if (qbig) {
+        if (!hm) return BRC_E_INVALID;
         if (perlink || mode == BRC_MODE_SPEC) return BRC_E_INVALID;
         if (mode == BRC_MODE_BEB) return launch_life_one<BRC_MODE_BEB, false, 8, true>(blocks, lds, s, P);
         if (mode == BRC_MODE_REFERENCE) return launch_life_one<BRC_MODE_REFERENCE, false, 8, true>(blocks, lds, s, P);

@@ -63,7 +63,8 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 // RW = 64 ring rows then (step statistics in 64 lanes, delivery bitmaps in a 64-row HBM ring).
 // QBIG: key windows of 64 / 128 (the reference protocol's many-round runs), two-class form only.  Both
 // are instantiations of their own, so the default ones keep their registers.
-template <int MODE, bool PL, int DLX = 8, bool QBIG = false>
+// HMT: the slot metadata in HBM (key windows >= 32, two-class form; QBIG implies it)
+template <int MODE, bool PL, int DLX = 8, bool QBIG = false, bool HMT = false>
 __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAVES : 6) : 8) void brc_life(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
@@ -84,16 +85,35 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     const bool seen_on = NV > 1;
 
     // ---- LDS carve (lds_bytes_life)
+    // Key windows >= 32 (the reference protocol's many-round runs; NK = 8192 slots at n = 64 and Q = 128) keep
+    // the slot metadata in HBM instead (P.lmeta, 32 KB per instance at Q = 128): in LDS it held 32 of the wave's
+    // 50 KB and capped the CU at 3 such waves.  Its accesses are few per key (the SEND claims the slot, the
+    // lifetime simulation stamps the slot's last step, the consensus pass reads a key word's values once into
+    // s_sv), against a lifetime of ~20 simulated steps
+    constexpr bool HM = QBIG || HMT;
+    static_assert(!(HM && PL), "HBM slot metadata: two-class form");
+    uint32_t* const g_meta = HM ? P.lmeta + item * (uint64_t)NK : nullptr;
     uint32_t* s_meta = (uint32_t*)smem;
+    uint32_t* s_sv = (uint32_t*)smem;             // HM: metadata snapshot of the key words being consumed [2][64]
     // two-class form: the step at which each receiver class delivers key slot k -- a class's honest
     // receivers evolve identically, so a class delivers a key once, at one step, whole.  One byte,
     // 0x80 | step mod 128 (0: none): a key's deliveries lie within 4 Dd <= 32 steps of its creation, and
     // the consensus pass clears the entries of the step it consumes (every entry's step is one it visits:
     // a delivery lands on an honest class, so its step has arrivals), so no stale entry aliases a later
     // step.  The per-link form keeps its deliveries in HBM (P.dring).
-    uint8_t* s_dA = (uint8_t*)(s_meta + NK);
+    uint8_t* s_dA = (uint8_t*)(s_meta + (HM ? 128u : NK));   // (PL: unused)
     uint8_t* s_dB = s_dA + NK;
-    uint64_t* s_hm = (uint64_t*)((char*)smem + ((4 * NK + (PL ? 0u : 2 * NK) + 7) & ~7u));   // REFERENCE / BEB: hosts per value [4][64]
+    uint64_t* s_hm = (uint64_t*)((char*)smem + ((4 * (HM ? 128u : NK) + (PL ? 0u : 2 * NK) + 7) & ~7u));   // REFERENCE / BEB: hosts per value [4][64]
+    // slot metadata word k: LDS, or (HM) this instance's HBM row through agent-scope relaxed atomics (L2-served,
+    // in program order for one location, as the delivery ring P.dring is accessed)
+    auto mld = [&](uint32_t k) -> uint32_t {
+        if (HM) return __hip_atomic_load(g_meta + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return s_meta[k];
+    };
+    auto mst = [&](uint32_t k, uint32_t v) {
+        if (HM) __hip_atomic_store(g_meta + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else s_meta[k] = v;
+    };
     uint64_t* s_seen = s_hm;                      // SPEC, NV > 1: [Q][64]
     uint32_t* s_cnt = (uint32_t*)(s_seen + (seen_on ? Q * 64 : 0u));   // SPEC: [Q][64]
 
@@ -173,7 +193,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) {
-        s_meta[i] = 0;
+        mst(i, 0u);
         if (!PL) { s_dA[i] = 0; s_dB[i] = 0; }
     }
     if constexpr (SPEC) {
@@ -216,9 +236,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // later step: nothing of the old key needs clearing.
     auto send_key_now = [&](uint32_t s, uint32_t v) {
         const uint32_t k = (d * NV) * Q + (s & Qm);
-        const uint32_t m = s_meta[k];
+        const uint32_t m = mld(k);
         if ((lm_s1(m) != 0 && t < lm_tend(m)) || s >= 0x3FFEu) { ovf = true; return; }
-        s_meta[k] = ((t + 1u) << 16) | ((v & 3u) << 14) | (s + 1u);   // busy until simulated
+        mst(k, ((t + 1u) << 16) | ((v & 3u) << 14) | (s + 1u));   // busy until simulated
         if constexpr (QBIG) {
             if (clr_n == 0) clr_s = s;
             ++clr_n;
@@ -249,7 +269,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         sq_n = 0; sq_v = 0;
     };
     // a slot's consensus view: value << 14 | (s + 1), as the BRB phase left it
-    auto snap = [&](uint32_t k) -> uint32_t { return s_meta[k] & 0xFFFFu; };
+    // (HM: the consensus passes read it from their s_sv snapshot of the word being consumed, snap_w)
+    auto snap = [&](uint32_t k) -> uint32_t { return mld(k) & 0xFFFFu; };
+    auto snap_w = [&](uint32_t k) -> uint32_t { return HM ? s_sv[k & 63u] : s_meta[k] & 0xFFFFu; };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {
             const uint32_t v = (order >> (2 * i)) & 3;
@@ -565,7 +587,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             rows |= (RowT)1 << row;
             last = ts;
         }
-        if (lane == 0) s_meta[k] = (s_meta[k] & 0xFFFFu) | (last << 16);
+        if (lane == 0) mst(k, (mld(k) & 0xFFFFu) | (last << 16));
     };
     // the keys created this step (every lane's clr_s .. clr_s + clr_n - 1), each simulated once
     auto simulate_new = [&]() {
@@ -657,23 +679,33 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
 #pragma unroll 1
             for (uint32_t w = 0; w < nkw; w += wpg) {
                 uint64_t gb[2] = {dword(w), wpg > 1 ? dword(w + 1) : 0ull};
+                if (!__ballot((gb[0] | gb[1]) != 0)) continue;
+                // the group's slot metadata, one coalesced read per word (no SEND changes it during the pass)
+                s_sv[lane] = mld(w * 64 + lane) & 0xFFFFu;
+                if (wpg > 1) s_sv[64 + lane] = mld((w + 1) * 64 + lane) & 0xFFFFu;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 while (gb[0] | gb[1]) {
                     uint32_t bs = 0xFFFFFFFFu, bk = 0;
                     for (uint32_t j = 0; j < wpg; ++j)
                         for (uint64_t x = gb[j]; x; x &= x - 1) {
                             const uint32_t kk = (w + j) * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1u;
-                            const uint32_t s1 = snap(kk) & 0x3FFFu;
+                            const uint32_t s1 = s_sv[kk - w * 64] & 0x3FFFu;
                             if (s1 < bs) { bs = s1; bk = kk; }
                         }
                     gb[(bk >> 6) - w] &= ~(1ull << (bk & 63));
-                    if constexpr (SPEC) spec_deliver(bk);
-                    else cons_deliver_vh(snap(bk) >> 14, bk >> ksh);
+                    static_assert(!(QBIG && SPEC), "QBIG: reference protocol");
+                    cons_deliver_vh(s_sv[bk - w * 64] >> 14, bk >> ksh);
                 }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
         } else
 #pragma unroll 1
         for (uint32_t w = 0; w < nkw; ++w) {
             uint64_t bits = dword(w);
+            if (HM && __ballot(bits != 0)) {           // the word's slot metadata, one coalesced read
+                s_sv[lane] = mld(w * 64 + lane) & 0xFFFFu;
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
             if constexpr (SPEC) {
                 // word at once when every delivering lane is at one phase index c0 and its current-phase
                 // deliveries cannot complete the phase (brc_step.h, SPEC consensus pass)
@@ -706,7 +738,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             } else {
                 // word at once when no phase can change (brc_step.h, REFERENCE consensus pass)
                 if (__ballot(bits != 0)) {
-                    const uint32_t sv = snap(w * 64 + lane) >> 14;
+                    const uint32_t sv = snap_w(w * 64 + lane) >> 14;
                     const uint64_t vm[4] = {__ballot(sv == 0), __ballot(sv == 1), __ballot(sv == 2), __ballot(sv == 3)};
                     const uint32_t nb = (uint32_t)__popcll(bits);
                     const bool oneper = (uint32_t)__popcll(fold_groups(bits, Q)) == nb;
@@ -743,14 +775,15 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     uint32_t bs = 0xFFFFFFFFu;
                     for (uint64_t x = grp; x; x &= x - 1) {
                         const uint32_t bb = __ffsll((unsigned long long)x) - 1;
-                        const uint32_t s1 = snap(w * 64 + bb) & 0x3FFFu;
+                        const uint32_t s1 = snap_w(w * 64 + bb) & 0x3FFFu;
                         if (s1 < bs) { bs = s1; best = bb; }
                     }
                 }
                 bits &= ~(1ull << best);
                 if constexpr (SPEC) spec_deliver(w * 64 + best);
-                else cons_deliver_vh(snap(w * 64 + best) >> 14, (w * 64 + best) >> ksh);
+                else cons_deliver_vh(snap_w(w * 64 + best) >> 14, (w * 64 + best) >> ksh);
             }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         defer = false;
@@ -809,9 +842,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     }
 }
 
-template <int MODE, bool PL, int DLX = 8, bool QBIG = false>
+template <int MODE, bool PL, int DLX = 8, bool QBIG = false, bool HMT = false>
 int launch_life_one(uint32_t blocks, uint32_t lds, hipStream_t s, const Params* P) {
-    auto kern = brc_life<MODE, PL, DLX, QBIG>;
+    auto kern = brc_life<MODE, PL, DLX, QBIG, HMT>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return BRC_E_HIP;

@@ -306,6 +306,43 @@ def test_cfg4_many_rounds_2p20_one_launch():
             assert r["last_decide_value"] == last[d] and r["decide_count"] == count[d] >= CAP, (g, d)
 
 
+@pytest.mark.parametrize("leg", ["long", "spec64"])
+def test_cfg4_round_cap_64_2p20_bench_legs(leg):
+    """bench.py's long and spec64 legs at their timed size: SURVEY cfg4's round cap 64 at the full 2^20
+    instances per GPU, one launch each.  long: the reference protocol (the re-proposal loop
+    core/byzantinerandomizedconsensus.py:96-106; by round 64 ~7,600 keys of one instance are live at
+    once, so the key-lifetime kernel with a key window of 128, its slot metadata in HBM).  spec64: the
+    intended protocol with the common coin (:88-92 made reachable) on the step kernel, window 8.
+    Sampled ids equal the oracle (counters incl. cell-steps, every replica's first and last decision
+    and its decide count)."""
+    L = _L()
+    N, CAP = 1 << 20, 64
+    spec = leg == "spec64"
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=CAP, step_cap=4000, key_window=8 if spec else 128, proposals=L.PROPOSALS_PHILOX,
+              mode=L.MODE_SPEC if spec else L.MODE_REFERENCE, coin_seed=0xC017C017)
+    ids = sorted(random.Random(6464 + spec).sample(range(N - 1), 5)) + [N - 1]
+    with _engine(instance_offset=0, instances=N, **kw) as eng:
+        eng.run()
+        assert eng.last_kernel() == ("step" if spec else "life")
+        st = eng.stats()
+        vals, dis = eng.decisions()
+        res = {i: eng.instances_result(i, 1)[0] for i in ids}
+        reps = {i: eng.replicas(i, 1)[0] for i in ids}
+    assert st["done"] == N and st["overflow"] == 0 and dis == 0
+    if spec:
+        specs = [S.spec_cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP, window=8, coin_seed=0xC017C017)
+                 for g in ids]
+    else:
+        specs = [S.cons_spec(64, 21, 0x5EED0004, 2, 8, g, round_cap=CAP) for g in ids]
+    for g, (exp, first, last, count) in zip(ids, _oracle_first_last(specs)):
+        for k in KEYS:
+            assert res[g][k] == exp[k], (g, k)
+        for d, r in enumerate(reps[g]):
+            assert (r["first_decide_round"], r["first_decide_t"], r["first_decide_value"]) == first[d], (g, d)
+            assert r["last_decide_value"] == last[d] and r["decide_count"] == count[d] >= CAP, (g, d)
+
+
 @pytest.mark.parametrize("model,dmax", [("slowset", 8), ("uniform", 2), ("uniform", 4), ("geometric", 16)])
 def test_cfg4_connection_peers_2p20_sampled(model, dmax):
     """cfg4 with connection-identity peers -- what the shipped reference runs

@@ -189,6 +189,30 @@ def test_lifetime_kernel_equals_step_kernel_and_oracle(name):
                 assert rep["decide_count"] == 0, (name, i, d)
 
 
+def test_lifetime_only_engine_rejects_injections_up_front():
+    """A sender-peer engine with a key window above 32 at n = 64 runs on the key-lifetime kernel only
+    (brc.h brc_last_kernel): the choice is fixed at brc_create (configuration and device model, not free
+    memory), brc_last_kernel reports it before any run, and brc_inject refuses at once
+    (BRC_E_UNSUPPORTED) instead of succeeding and failing the later run; so does a stepped run."""
+    from byzantinerandomizedconsensus_amd.engine import Engine
+    L = _L()
+    kw = dict(n=64, f=21, protocol="consensus", seed=0x5EED0004, delay_model=L.DELAY_SLOWSET, delay_max=8,
+              round_cap=2, step_cap=4000, key_window=64, proposals=L.PROPOSALS_PHILOX)
+    with Engine(instances=4, **kw) as eng:
+        assert eng.last_kernel() == "life"
+        with pytest.raises(L.EngineError) as ei:
+            eng.inject([dict(t=0, kind=L.INJ_PROPOSE, instance=0, node=0, value=1)])
+        assert ei.value.code == L.E_UNSUPPORTED
+        with pytest.raises(L.EngineError) as ei:
+            eng.run(5)
+        assert ei.value.code == L.E_UNSUPPORTED
+        eng.run()
+        assert eng.last_kernel() == "life"
+        assert all(r["status"] == "done" for r in eng.instances_result())
+    with Engine(instances=4, **dict(kw, key_window=8)) as eng:
+        assert eng.last_kernel() == "step"
+
+
 def test_kernel_choice():
     """Default choice: connection peers run on the lifetime kernel, sender peers on the step kernel
     (faster there); event logs, injections, stepped runs and two-class delays past 8 stay on the step kernel;

@@ -27,6 +27,11 @@ Legs, one JSON line (rank 0); each leg is one launch per step at 2^20 instances:
   many       the reference protocol run to round cap 8 (SURVEY cfg4's "many rounds"): by round 8
              ~1,000 keys of one instance are live at once (phase leakage), more than any cell store
              holds at 2^20, so the engine runs it on the key-lifetime kernel (key window 32).
+  long       the reference protocol to SURVEY cfg4's round cap 64 (key window 128: ~7,600 keys of one
+             instance live at once by round 64), key-lifetime kernel, 2^20 instances in one launch.
+  spec64     SPEC to round cap 64: 64 decisions per replica, coin rounds included, step kernel.
+The legs of seconds per step (many, long, spec64) time at most LEG_STEPS of --steps / --warmup
+and report the counts they timed.
 """
 import argparse
 import json
@@ -55,6 +60,9 @@ LEGS = {"reference": ("reference", "sender", "slowset", DELAY_MAX, 4),
         "spec64": ("spec", "sender", "slowset", DELAY_MAX, 8)}
 # legs with a round cap of their own (the others take --round-cap)
 LEG_CAP = {"many": MANY_CAP, "long": LONG_CAP, "spec64": LONG_CAP}
+# legs of seconds per step time at most this many (steps, warmup) of --steps / --warmup, so that the default
+# run stays within minutes; every leg reports the steps it timed
+LEG_STEPS = {"many": (3, 1), "long": (1, 0), "spec64": (1, 0)}
 
 
 def parse():
@@ -63,10 +71,11 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
-    ap.add_argument("--legs", default="reference,spec,conn,connu,many",
+    ap.add_argument("--legs", default="reference,spec,conn,connu,many,long,spec64",
                     help="comma list of reference (the headline value), spec (SURVEY §8 F3 coin rounds), conn "
                          "(connection-identity peers, what the shipped reference runs: SURVEY §8 F1), connu (the same "
-                         "under per-link uniform[1,2] delays) and many (the reference protocol to round cap 8)")
+                         "under per-link uniform[1,2] delays), many (the reference protocol to round cap 8), long (the "
+                         "reference protocol to SURVEY cfg4's round cap 64) and spec64 (SPEC to round cap 64)")
     ap.add_argument("--mode", choices=tuple(LEGS), default=None,
                     help="shorthand for --legs <mode> (the headline leg is the first one run)")
     ap.add_argument("--round-cap", type=int, default=1, help="round cap of every leg but many")
@@ -207,12 +216,15 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
 
     kern = set()
 
-    for _ in range(args.warmup):
+    steps, warmup = args.steps, args.warmup
+    if mode in LEG_STEPS:
+        steps, warmup = min(steps, LEG_STEPS[mode][0]), min(warmup, LEG_STEPS[mode][1])
+    for _ in range(warmup):
         one_step()
     barrier()
     t0 = time.perf_counter()
     kms = []
-    for _ in range(args.steps):
+    for _ in range(steps):
         kms.append(one_step())
     barrier()
     elapsed = time.perf_counter() - t0
@@ -283,15 +295,17 @@ def run_leg(args, mode, world, rank, local, dist, coll_dev):
         if prof.get("issue"):
             roof["issue"] = prof["issue"]
     leg = {
-        "value": decided * args.steps / elapsed,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "value": decided * steps / elapsed,
+        "ms_per_step": elapsed / steps * 1e3,
+        "steps": steps,
+        "warmup": warmup,
         "kernel_ms": kernel_ms,
         "launches_per_step": launches,
         "decided_fraction": decided / float(per * world),
         "decide_round_hist": {str(r): c for r, c in enumerate(hist) if c},
         "decided_value_hist": {k: st["dec_" + k] for k in ("-1", "0", "1", "3", "undecided") if st["dec_" + k]},
         "agreement_violations": st["disagreements"],
-        "replica_message_steps_per_s": arrivals * args.steps / elapsed,
+        "replica_message_steps_per_s": arrivals * steps / elapsed,
         "counts": {k: st[k] for k in ("instances", "decided", "msgs_sent", "arrivals", "cell_steps", "deliveries",
                                       "decide_rounds_sum", "lane_loads", "max_t")},
         "roofline": roof,

@@ -10,7 +10,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libbrc_hip.so"
 LIB_PATH = os.environ.get("BRC_LIB") or os.path.join(_HERE, LIB_NAME)   # BRC_LIB: dev A/B builds only
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 OK, E_INVALID, E_NOMEM, E_HIP, E_UNSUPPORTED, E_STATE = 0, -1, -2, -3, -4, -5
 ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP error",
@@ -18,6 +18,7 @@ ERRORS = {E_INVALID: "invalid argument", E_NOMEM: "out of memory", E_HIP: "HIP e
 
 PROTO_BRB, PROTO_CONSENSUS = 0, 1
 MODE_REFERENCE, MODE_SPEC, MODE_BEB = 0, 1, 2
+FLAG_GENERAL_KEYS = 1       # brc.h BRC_FLAG_GENERAL_KEYS (ABI v7)
 PEER_SENDER, PEER_CONNECTION = 0, 1
 DELAY_CONST, DELAY_UNIFORM, DELAY_SLOWSET, DELAY_GEOMETRIC = 0, 1, 2, 3
 PROPOSALS_NONE, PROPOSALS_PHILOX, PROPOSALS_LOADED = 0, 1, 2
@@ -59,7 +60,7 @@ class Config(ctypes.Structure):
                 ("byz_pattern", ctypes.c_uint32), ("event_capacity", ctypes.c_uint32),
                 ("byzantine_mask", ctypes.c_uint64), ("device", ctypes.c_int32),
                 ("mode", ctypes.c_uint32), ("coin_seed", ctypes.c_uint64),
-                ("byzantine_mask_hi", ctypes.c_uint64 * 3), ("reserved", ctypes.c_uint32 * 4)]
+                ("byzantine_mask_hi", ctypes.c_uint64 * 3), ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 3)]
 
 
 class Injection(ctypes.Structure):

@@ -147,6 +147,7 @@ struct Engine {
     bool wide_wv4 = false;                       // wide: the 4-waves-per-SIMD instantiations (brc_step_wide.h WV)
     bool regmask = false;                        // NPAD = 64 lean kernel with register delay masks (NLR = 2)
     bool compact = false;                        // lean kernels (NPAD = 64, sender peers): u32 cells (C32_*)
+    bool general = false;                        // BRC_FLAG_GENERAL_KEYS at NPAD = 64 (KMODE_XREF)
     uint32_t lpi = 64;                           // replica lanes per item (64, or NPAD when wide)
     uint32_t bw = 1;                             // Byzantine-mask words per instance
     uint32_t NK = 0, nkw = 0, msize = 0, lds_bytes = 0;
@@ -399,7 +400,10 @@ int brc_create(const brc_config* cfg, void** out) {
         c.key_window * c.variants > ((c.mode != BRC_MODE_SPEC && c.n <= 64) ? 128u : 8u) ||
         c.f >= c.n || (c.byz_pattern == BRC_BYZ_EQUIVOCATE && c.variants < 2) ||
         (c.byz_pattern != BRC_BYZ_NONE && c.byz_pattern != BRC_BYZ_EQUIVOCATE) ||
-        c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB ||
+        c.proposals > BRC_PROPOSALS_LOADED || c.mode > BRC_MODE_BEB || (c.flags & ~(uint32_t)BRC_FLAG_GENERAL_KEYS) ||
+        // the general form at NPAD = 64 with sender peers is the reference protocol's (KMODE_XREF)
+        ((c.flags & BRC_FLAG_GENERAL_KEYS) && c.n > 32 && c.n <= 64 && c.peer_mode == BRC_PEER_SENDER &&
+         c.mode != BRC_MODE_REFERENCE) ||
         (c.n > 64 && c.mode == BRC_MODE_SPEC && c.variants != 1))
     {
         g_create_err = "invalid configuration (see include/brc.h field ranges)";
@@ -425,8 +429,10 @@ int brc_create(const brc_config* cfg, void** out) {
     e->nitems = (c.instances + e->ipw - 1) / e->ipw;
     const bool spec = c.mode == BRC_MODE_SPEC;
     const uint32_t nL = delay_values(c.delay_model, c.delay_max);
-    e->regmask = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && nL <= 2;
-    e->compact = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER;   // = lean_kernel<64, mode> (brc_step.h)
+    // BRC_FLAG_GENERAL_KEYS: NPAD = 64 with sender peers on the general form (KMODE_XREF), not the lean one
+    e->general = (c.flags & BRC_FLAG_GENERAL_KEYS) && e->npad == 64 && c.peer_mode == BRC_PEER_SENDER;
+    e->regmask = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && nL <= 2 && !e->general;
+    e->compact = e->npad == 64 && c.peer_mode == BRC_PEER_SENDER && !e->general;   // = lean_kernel<64, mode> (brc_step.h)
     // wide exchange words per (key, type): connection peers send 8 count planes per link delay
     const uint32_t xw = c.peer_mode == BRC_PEER_CONNECTION ? 8u * nL : xwords_wide(c.delay_model, c.delay_max, e->dm);
     e->lds_bytes = e->wide ? lds_bytes_wide(e->npad, e->NK, e->nkw, xw,
@@ -454,7 +460,7 @@ int brc_create(const brc_config* cfg, void** out) {
         e->life_pl = c.delay_model == BRC_DELAY_UNIFORM || c.delay_model == BRC_DELAY_GEOMETRIC;
         e->life_lds = lds_bytes_life(e->NK, spec, c.key_window, c.variants, e->life_pl);
         e->life_rw = (e->life_pl && c.delay_max > 8) ? LIFE_RW16 : LIFE_RW;
-        const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS &&
+        const bool eligible = e->npad == 64 && c.protocol == BRC_PROTO_CONSENSUS && !e->general &&
                               c.proposals != BRC_PROPOSALS_NONE && c.event_capacity == 0 && c.byz_pattern == BRC_BYZ_NONE &&
                               c.delay_max <= (e->life_pl ? 16u : 8u) && e->life_lds <= 160 * 1024 &&
                               // per-link form: its HBM delivery ring is [RW][NK] bits per instance
@@ -821,7 +827,7 @@ int brc_run(void* h, uint32_t max_steps, uint32_t* running_left) {
     HIPCHK(e, hipMemcpyAsync(e->dparams, &e->hparams, sizeof(Params), hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemsetAsync(e->gcount + 6, 0, 8, e->stream));   // instances still running after this launch
     HIPCHK(e, hipEventRecord(e->ev0, e->stream));   // times the step kernel alone
-    const int kmode = c.peer_mode == BRC_PEER_CONNECTION ? KMODE_CONN : (int)c.mode;
+    const int kmode = c.peer_mode == BRC_PEER_CONNECTION ? KMODE_CONN : e->general ? KMODE_XREF : (int)c.mode;
     e->fresh = false;
     e->last_life = life;
     if (life) {

@@ -41,6 +41,8 @@ constexpr int CHUNK_W = BRC_CHUNK_W;                // wide kernel: keys whose b
 // wide kernel: delivery-bitmap words per receiver = key-list positions per pass / 64
 __host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw < BRC_WIDE_DCW ? nkw : BRC_WIDE_DCW; }
 constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
+constexpr int KMODE_XREF = 4;               // ... reference protocol, sender peers, NPAD = 64 in the general
+                                            // (non-lean) form: BRC_FLAG_GENERAL_KEYS
 #ifndef BRC_CHUNK
 #define BRC_CHUNK 4
 #endif

@@ -400,7 +400,7 @@ __device__ __forceinline__ uint32_t pk2(uint32_t x) { return x | (x << 16); }   
 // [8..11] lean key-steps: processed, without arrivals, reaching only delivered cells, fully updated
 __device__ unsigned long long brc_stamps[BRC_NSTAMPS];
 #endif
-template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN; }
+template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN && MODE != KMODE_XREF; }
 
 template <int NPAD, int DM, bool EV, int MODE, int NLR>
 __global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? (MODE == BRC_MODE_SPEC ? BRC_MIN_WAVES_LEAN_SPEC
@@ -2225,6 +2225,16 @@ int launch_step(int dm, bool events, int mode, uint32_t blocks, uint32_t lds, hi
                                                      : launch_one<NPAD, 8, false, KMODE_CONN>(blocks, lds, s, P);
     if (mode == KMODE_CONN && dm == 16) return events ? launch_one<NPAD, 16, true, KMODE_CONN>(blocks, lds, s, P)
                                                       : launch_one<NPAD, 16, false, KMODE_CONN>(blocks, lds, s, P);
+    if constexpr (NPAD == 64) {
+        // BRC_FLAG_GENERAL_KEYS: the reference protocol with sender peers on the general (non-lean) form
+        if (mode == KMODE_XREF && dm == 4) return events ? launch_one<NPAD, 4, true, KMODE_XREF>(blocks, lds, s, P)
+                                                         : launch_one<NPAD, 4, false, KMODE_XREF>(blocks, lds, s, P);
+        if (mode == KMODE_XREF && dm == 8) return events ? launch_one<NPAD, 8, true, KMODE_XREF>(blocks, lds, s, P)
+                                                         : launch_one<NPAD, 8, false, KMODE_XREF>(blocks, lds, s, P);
+        if (mode == KMODE_XREF && dm == 16) return events ? launch_one<NPAD, 16, true, KMODE_XREF>(blocks, lds, s, P)
+                                                          : launch_one<NPAD, 16, false, KMODE_XREF>(blocks, lds, s, P);
+    }
+    if (mode == KMODE_XREF) return BRC_E_INVALID;
 #define BRC_CASE(DMX)                                                                                  \
     if (dm == DMX) {                                                                                   \
         if (mode == BRC_MODE_SPEC) return events ? launch_one<NPAD, DMX, true, BRC_MODE_SPEC>(blocks, lds, s, P) : launch_one<NPAD, DMX, false, BRC_MODE_SPEC>(blocks, lds, s, P); \

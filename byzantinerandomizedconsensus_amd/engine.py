@@ -27,7 +27,8 @@ class Engine:
     def __init__(self, n, f, instances, protocol="consensus", seed=0, delay_model=L.DELAY_CONST,
                  delay_max=1, delay_const=1, round_cap=1, step_cap=4000, key_window=4, variants=1,
                  proposals=L.PROPOSALS_NONE, byz_pattern=L.BYZ_NONE, byzantine=(), event_capacity=0,
-                 instance_offset=0, device=0, mode=L.MODE_REFERENCE, coin_seed=0, peer_mode=L.PEER_SENDER):
+                 instance_offset=0, device=0, mode=L.MODE_REFERENCE, coin_seed=0, peer_mode=L.PEER_SENDER,
+                 general_keys=False):
         self._lib = L.load()
         self._h = ctypes.c_void_p()
         mask = 0
@@ -39,7 +40,8 @@ class Engine:
                             delay_max=delay_max, delay_const=delay_const, round_cap=round_cap,
                             step_cap=step_cap, key_window=key_window, variants=variants,
                             proposals=proposals, byz_pattern=byz_pattern, event_capacity=event_capacity,
-                            byzantine_mask=mask & M64, device=device, mode=mode, coin_seed=coin_seed)
+                            byzantine_mask=mask & M64, device=device, mode=mode, coin_seed=coin_seed,
+                            flags=L.FLAG_GENERAL_KEYS if general_keys else 0)
         for w in range(3):
             self.cfg.byzantine_mask_hi[w] = (mask >> (64 * (w + 1))) & M64
         rc = self._lib.brc_create(ctypes.byref(self.cfg), ctypes.byref(self._h))

@@ -22,15 +22,14 @@ Deviations from the reference, all reported by exceptions and never silent:
   ``core/byzantinerandomizedconsensus.py:102-106``).  Clusters stop once every node has
   decided ``round_cap`` times (``configure``).
 * At most seven distinct proposal strings besides ``"-1"`` (three-bit value ids) -- three on
-  clusters of 33..64 nodes with ``peer_mode="sender"`` and above 64 nodes, whose kernels keep
-  two-bit ids.
+  clusters above 64 nodes (and best-effort broadcast above 32), whose kernels keep two-bit ids.
 * A payload SENT by two different origins (or SENT again) is one key in the reference (its
   dicts are keyed by the payload string); the engine models it as one key with extra SENDs
   (brc_step.h extra-SEND records: up to 16 per wave item, shared by the instances packed into
-  it) on clusters up to 32 nodes and with connection peers up to 64; on the others (33..64
-  nodes with sender peers, more than 64) a second origin raises ``EngineError``.  A node that
-  SENDs its own payload again with sender peers is a no-op everywhere: the network drops a
-  duplicate on every link (tests/golden/refharness.py).
+  it) on clusters up to 64 nodes (33..64 nodes with sender peers run the narrow kernel's general
+  form for this, brc.h BRC_FLAG_GENERAL_KEYS); above 64 nodes a second origin raises
+  ``EngineError``.  A node that SENDs its own payload again with sender peers is a no-op
+  everywhere: the network drops a duplicate on every link (tests/golden/refharness.py).
 * ``broadcast(type, m)`` takes SEND, ECHO and READY (the reference also puts other types on
   the wire, which its handler then ignores): other types raise ``EngineError``.
 * Peer addresses in ``peer_list`` without a constructed node in this process are silent
@@ -163,8 +162,9 @@ class Cluster:
         self.sent = set()          # keys SENT (a payload may be declared first by an ECHO / READY)
         # three-bit value ids on the narrow kernels that keep them (include/brc.h brc_injection.value)
         n = len(peers)
-        # the lean (33..64 nodes, sender peers) and wide (> 64) kernels: two-bit value ids, one SEND per key
-        self.lean_or_wide = n > 64 or (n > 32 and cfg["peer_mode"] == "sender")
+        # the wide kernel (> 64 nodes): two-bit value ids, one SEND per key.  33..64 nodes with sender peers
+        # run the narrow kernel's general form (BRC_FLAG_GENERAL_KEYS), which keeps what n <= 32 keeps
+        self.lean_or_wide = n > 64
         self.values = ValueTable(4 if self.lean_or_wide else 8)
         self.engine = None
         self.seen_events = 0
@@ -295,7 +295,8 @@ class Cluster:
                              key_window=8, variants=1, byzantine=silent,
                              event_capacity=c["event_capacity"], instance_offset=c["instance_id"],
                              device=c["device"], mode=L.MODE_BEB if self.beb else L.MODE_REFERENCE,
-                             peer_mode=L.PEER_SENDER if self.beb else PEER_MODES[c["peer_mode"]])
+                             peer_mode=L.PEER_SENDER if self.beb else PEER_MODES[c["peer_mode"]],
+                             general_keys=not self.beb)
 
     def _flush(self):
         if self.actions:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define BRC_ABI_VERSION 6
+#define BRC_ABI_VERSION 7
 
 enum {
     BRC_OK = 0,
@@ -104,8 +104,16 @@ typedef struct {
     uint32_t mode;            /* BRC_MODE_* */
     uint64_t coin_seed;       /* BRC_MODE_SPEC: common-coin key */
     uint64_t byzantine_mask_hi[3];  /* replicas 64..255 that run no code */
-    uint32_t reserved[4];
+    uint32_t flags;           /* BRC_FLAG_* */
+    uint32_t reserved[3];
 } brc_config;
+/* BRC_FLAG_GENERAL_KEYS (v7): at n in 33..64 with sender peers and the reference protocol, run the
+ * narrow kernel's general form instead of the lean one -- 8-B cells with generation tags, 3-bit value
+ * ids (7 proposal strings besides "-1") and extra SENDs of one key (one payload SENT by several
+ * origins, core/brbroadcast.py:74-79 keys by the payload string) -- what n <= 32 and connection peers
+ * always have.  For the class API's single-instance clusters; the batched workloads keep the lean
+ * kernels (4-B cells, 2-bit ids). */
+enum { BRC_FLAG_GENERAL_KEYS = 1 };
 
 typedef struct {
     uint32_t t;               /* action time: performed after step t, messages stamped t */

@@ -25,7 +25,7 @@ def _cfg_key(sp):
     return (sp["n"], sp["f"], sp["mode"], sp.get("nv", 1), sp["seed"], sp["delay_model"], sp["dmax"],
             sp.get("dconst", 1), sp.get("round_cap", 0), sp.get("step_cap", 10000),
             tuple(sorted(sp.get("byzantine", []))), sp.get("window"), sp.get("coin_seed"), sp.get("peer_mode", "sender"),
-            sp.get("key_window"))
+            sp.get("key_window"), sp.get("general_keys", False))
 
 
 def _injections(sp, local):
@@ -79,7 +79,7 @@ def run_batch(specs, key_window=None, event_capacity=1 << 21, device=0):
                  variants=sp0.get("nv", 1), byzantine=sp0.get("byzantine", ()), event_capacity=event_capacity,
                  instance_offset=sp0["g"], device=device, mode=mode,
                  peer_mode=L.PEER_CONNECTION if sp0.get("peer_mode") == "connection" else L.PEER_SENDER,
-                 coin_seed=sp0.get("coin_seed", 0))
+                 coin_seed=sp0.get("coin_seed", 0), general_keys=sp0.get("general_keys", False))
     try:
         inj = []
         for i, sp in enumerate(specs):

@@ -335,6 +335,7 @@ def scenario_groups():
                                    for g in range(1)]
     G.update(values8_specs())
     G.update(multisend_specs())
+    G.update(general_keys_specs())
     for name, specs in G.items():
         for i, sp in enumerate(specs):
             sp.setdefault("name", "%s/%d" % (name, i))
@@ -361,6 +362,29 @@ def multisend_specs():
                                        extra=crash[:14] + [dict(t=2, kind="brb_send", node=3, kp=7, s=0,
                                                                 payload="TEST 8.0")])
                               for g, (m, d) in enumerate(((1, 4), (2, 8), (3, 6)))]
+    return G
+
+
+def general_keys_specs():
+    """33..64 nodes with sender peers and what the reference keys by the payload string (core/brbroadcast.py:
+    74-79, core/byzantinerandomizedconsensus.py:57-60): five proposal strings, one payload SENT by two origins
+    and again by its own.  The engine runs them on the narrow kernel's general form (brc.h
+    BRC_FLAG_GENERAL_KEYS; the lean kernel keeps 2-bit value ids and one SEND per key): general_keys."""
+    G = {}
+    extra = [dict(t=0, kind="brb_send", node=9, kp=0, s=0, payload="TEST 1.0"),      # a second origin
+             dict(t=0, kind="brb_send", node=0, kp=0, s=0, payload="TEST 1.0"),      # its own origin again
+             dict(t=0, kind="brb_send", node=21, kp=2, s=0, payload="TEST 3.0")]
+    G["brb_multisend_n40"] = [dict(brb_spec(40, 13, 0x4A10 + g, m, d, g, [(0, 0, 0), (0, 1, 0), (0, 2, 0)],
+                                            extra=extra), general_keys=True)
+                              for g, (m, d) in enumerate(((0, 1), (1, 3), (2, 4)))]
+    # ids 1..5 = "0", "1", "3", "alpha", "beta": a majority of a new string, a five-way split ("-1"), a
+    # majority of "beta" with every other string present
+    pats = [[4] * 30 + [1, 2, 3, 5] * 2 + [5, 5],
+            [1, 2, 3, 4, 5] * 8,
+            [5] * 29 + [1, 2, 3, 4] * 2 + [4, 3, 2]]
+    G["cons_values_n40"] = [dict(cons_spec(40, 7, 0x4A20 + g, m, d, g, round_cap=2, proposals=pats[g]),
+                                 values=VALUES8, general_keys=True)
+                            for g, (m, d) in enumerate(((0, 1), (1, 3), (2, 4)))]
     return G
 
 

@@ -166,7 +166,7 @@ def test_cluster_value_table_width():
     """Clusters get three-bit value ids where their kernel keeps them (include/brc.h)."""
     network.reset()
     try:
-        for n, pm, cap in ((7, "connection", 8), (16, "sender", 8), (40, "connection", 8), (40, "sender", 4),
+        for n, pm, cap in ((7, "connection", 8), (16, "sender", 8), (40, "connection", 8), (40, "sender", 8),
                            (70, "connection", 4)):
             c = network.Cluster(tuple(("localhost", 9000 + i) for i in range(n)), dict(network.settings(), peer_mode=pm))
             assert c.values.cap == cap, (n, pm)
@@ -174,10 +174,11 @@ def test_cluster_value_table_width():
         network.reset()
 
 
-def test_repeat_send_on_lean_cluster():
-    """33..64 nodes with sender peers (the lean kernel: one SEND per key): a node SENDing its own
-    payload again is a duplicate on every link -- the reference network carries nothing
-    (tests/golden/refharness.py) -- so it is a no-op; a second origin of the payload is refused."""
+def test_repeat_send_on_general_and_wide_clusters():
+    """33..64 nodes with sender peers run the narrow kernel's general form (brc.h BRC_FLAG_GENERAL_KEYS):
+    a payload SENT again by its node or by a second origin is one key with extra SENDs, as on <= 32
+    nodes (the engine drops a sender's repeat on every link it used, as the reference network does).
+    Above 64 nodes (the wide kernel: one SEND per key) a repeat is refused."""
     from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
     network.reset()
     try:
@@ -185,12 +186,10 @@ def test_repeat_send_on_lean_cluster():
         peers = _peers(40, 7100)
         nodes = [BRBroadcast(40, 13, p, peers, None) for p in peers]
         nodes[5].broadcast(BRBroadcast.SEND, "A")
-        nodes[5].broadcast(BRBroadcast.SEND, "A")        # the same node again: dropped on every link
+        nodes[5].broadcast(BRBroadcast.SEND, "A")        # the same node again: an extra SEND, dropped by the engine
+        nodes[6].broadcast(BRBroadcast.SEND, "A")        # a second origin: one key, two SENDs
         c = nodes[0].cluster
-        assert [(a["node"], a["kp"], a["s"]) for a in c.actions] == [(5, 5, 0)]
-        with pytest.raises(L.EngineError):
-            nodes[6].broadcast(BRBroadcast.SEND, "A")    # a second origin: one key, two SENDs
-        assert len(c.actions) == 1
+        assert [(a["node"], a["kp"], a["s"]) for a in c.actions] == [(5, 5, 0), (5, 5, 0), (6, 5, 0)]
         network.reset()
         network.configure(peer_mode="connection")        # connection peers: a repeat travels again
         peers = _peers(70, 7200)
@@ -310,7 +309,7 @@ def test_direct_deliver_calls_match_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("group", ["brb_usermsg_n7", "conn_brb_usermsg_n7"])
+@pytest.mark.parametrize("group", ["brb_usermsg_n7", "conn_brb_usermsg_n7", "brb_multisend_n40"])
 def test_user_echo_ready_broadcasts_match_reference(group):
     """Honest nodes' user code issues ECHO / READY broadcasts (base/broadcast.py:17): an early ECHO
     of a SENT payload, ECHO / READY of payloads nobody SENDs (f + 1 READYs -> amplification ->
@@ -347,10 +346,11 @@ def test_user_echo_ready_broadcasts_match_reference(group):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("group", ["cons_values_n7", "conn_cons_values_n7"])
+@pytest.mark.parametrize("group", ["cons_values_n7", "conn_cons_values_n7", "cons_values_n40"])
 def test_more_than_three_proposal_strings_match_reference(group):
     """Seven proposal strings besides "-1" (three-bit value ids): the decide upcalls equal the
-    reference's (tests/golden/<group>.json, made by the reference classes), both peer modes."""
+    reference's (tests/golden/<group>.json, made by the reference classes), both peer modes; five
+    strings at n = 40 with sender peers (the general form, brc.h BRC_FLAG_GENERAL_KEYS)."""
     from byzantinerandomizedconsensus_amd.base.consensus import IConsensusHandler
     from byzantinerandomizedconsensus_amd.core.byzantinerandomizedconsensus import ByzantineRandomizedConsensus
     for case in GROUPS[group]:
@@ -382,10 +382,10 @@ def test_more_than_three_proposal_strings_match_reference(group):
 
 
 def test_repeated_send_refused_where_the_kernel_keeps_one_send_per_key():
-    """Clusters of 33..64 nodes with sender peers (lean kernel) and above 64 nodes (wide kernel)
-    model one SEND per key: a payload SENT again, or by a second node, raises before any engine call."""
+    """Clusters above 64 nodes (wide kernel) model one SEND per key: a payload SENT again, or by a
+    second node, raises before any engine call; up to 64 nodes it is an extra SEND."""
     from byzantinerandomizedconsensus_amd.core.brbroadcast import BRBroadcast
-    for n, pm, ok in ((40, "sender", False), (40, "connection", True), (70, "connection", False), (16, "sender", True)):
+    for n, pm, ok in ((40, "sender", True), (40, "connection", True), (70, "connection", False), (16, "sender", True)):
         network.reset()
         network.configure(peer_mode=pm)
         try:

@@ -47,14 +47,15 @@ def _run(cmd, timeout):
 
 def _legs(d):
     out = {"reference": {k: d[k] for k in KEYS}}
-    for leg in ("spec", "many"):
-        out[leg] = {k: d[leg + "_leg"][k] for k in KEYS}
+    for leg in ("spec", "many", "long", "spec64"):
+        if leg + "_leg" in d:
+            out[leg] = {k: d[leg + "_leg"][k] for k in KEYS}
     return out
 
 
 @pytest.mark.gpu
 def test_two_ranks_equal_one_rank_over_the_same_global_ids():
-    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many"]
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many,long,spec64"]
     multi = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(WORLD),
                   "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
                   "--gpus", str(WORLD), "--backend", "gloo", "--instances", str(PER_RANK)] + bench_args, 300)
@@ -62,7 +63,7 @@ def test_two_ranks_equal_one_rank_over_the_same_global_ids():
     assert multi["n_gpus"] == WORLD and single["n_gpus"] == 1
     assert multi["config"]["instances_per_gpu"] * WORLD == single["config"]["instances_per_gpu"]
     m, s = _legs(multi), _legs(single)
-    for leg in ("reference", "spec", "many"):
+    for leg in ("reference", "spec", "many", "long", "spec64"):
         assert m[leg]["counts"]["instances"] == PER_RANK * WORLD
         assert m[leg]["counts"]["decided"] > 0
         assert m[leg] == s[leg], leg

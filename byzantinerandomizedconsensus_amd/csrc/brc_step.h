@@ -402,10 +402,17 @@ __device__ unsigned long long brc_stamps[BRC_NSTAMPS];
 #endif
 template <int NPAD, int MODE> constexpr bool lean_kernel() { return NPAD == 64 && MODE != KMODE_CONN && MODE != KMODE_XREF; }
 
+// Event-log instantiations (EV) run the class API's single-instance clusters and the parity tests' small
+// batches, never a bandwidth workload: they take BRC_MIN_WAVES_EV waves per SIMD (256 VGPRs) so the event
+// code spills nothing (at 128 VGPRs the n = 4 connection-peer kernel spilled 126 VGPRs to scratch)
+#ifndef BRC_MIN_WAVES_EV
+#define BRC_MIN_WAVES_EV 2
+#endif
 template <int NPAD, int DM, bool EV, int MODE, int NLR>
-__global__ __launch_bounds__(64 * WPB, (lean_kernel<NPAD, MODE>() ? (MODE == BRC_MODE_SPEC ? BRC_MIN_WAVES_LEAN_SPEC
-                                                                                          : BRC_MIN_WAVES_LEAN)
-                                                                : BRC_MIN_WAVES))
+__global__ __launch_bounds__(64 * WPB, (EV ? BRC_MIN_WAVES_EV
+                                           : lean_kernel<NPAD, MODE>() ? (MODE == BRC_MODE_SPEC ? BRC_MIN_WAVES_LEAN_SPEC
+                                                                                              : BRC_MIN_WAVES_LEAN)
+                                                                       : BRC_MIN_WAVES))
 void brc_step(const Params* __restrict__ pp) {
     // Parameters live in device memory, not in kernarg: the loop's global stores may alias
     // them, so the compiler re-reads cold fields (scalar loads) where they are used instead of
@@ -1586,7 +1593,9 @@ void brc_step(const Params* __restrict__ pp) {
             }
         };
         // xsa: this lane's extra-SEND arrivals of key k (the pre-pass below; 0 in the key loop)
-        auto process = [&](const uint32_t k, const uint64_t wd, const uint32_t xsa) {
+        // always inlined: an outlined call (the event-log instantiations' choice) keeps every variable it
+        // captures by reference in scratch memory
+        auto process = [&](const uint32_t k, const uint64_t wd, const uint32_t xsa) __attribute__((always_inline)) {
             // both LDS reads issue before either is waited on (k == NK, the trash row: junk, unused)
             const uint64_t m_raw = s_meta[mbase + k];
             const uint32_t gw_raw = s_gen[mbase + k];

@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 // 128 VGPRs, and with the DM-sized ring and 2-word delivery bitmaps a cfg5 workgroup fits 40 KB of LDS, so
 // four workgroups share a CU (cfg5 const: 37.8 -> 31.9 ms, A/B round 5; uniform planes lose: 137.7 -> 139.8)
 template <int NPAD, int DM, bool EV, int MODE, int WV = 0>
-__global__ __launch_bounds__(NPAD, (WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES)) void brc_step_wide(const Params* __restrict__ pp) {
+__global__ __launch_bounds__(NPAD, (EV ? BRC_MIN_WAVES_EV : WV ? WV : DM == 16 ? BRC_WIDE_WAVES16 : BRC_WIDE_WAVES)) void brc_step_wide(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     // u64 words per cell: CONN adds the lane's ECHO and READY send-count rings (Ring16, brc_step.h)

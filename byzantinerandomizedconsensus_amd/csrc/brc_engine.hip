@@ -686,13 +686,17 @@ int brc_inject(void* h, const brc_injection* list, size_t count) {
         }
         const uint64_t item = x.instance / e->ipw;
         if (its[item].initialized != 0 && x.t < its[item].t) { e->err = "injection time is before the instance's current step"; return BRC_E_STATE; }
-        if (drop) continue;                      // carried on no link: changes no instance state
         if (ist[x.instance].status == BRC_QUIESCENT && e->life_done) {
             e->err = "instance finished by the key-lifetime kernel (no step state to resume): brc_reset first";
             return BRC_E_STATE;
         }
+        if (ist[x.instance].status != BRC_QUIESCENT && ist[x.instance].status != BRC_RUNNING) {
+            e->err = "instance already stopped"; return BRC_E_STATE;
+        }
+        // a repeated SEND carried on no link (sender peers) changes no instance state: accepted, not staged
+        // (after the stopped-instance checks: a stopped instance refuses it like every other injection)
+        if (drop) continue;
         if (ist[x.instance].status == BRC_QUIESCENT) reopen.push_back(x.instance);
-        else if (ist[x.instance].status != BRC_RUNNING) { e->err = "instance already stopped"; return BRC_E_STATE; }
         staged.push_back(r);
         staged_item.push_back(item);
     }

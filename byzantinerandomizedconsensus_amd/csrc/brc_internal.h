@@ -40,6 +40,13 @@ constexpr int CHUNK_W = BRC_CHUNK_W;                // wide kernel: keys whose b
 #endif
 // wide kernel: delivery-bitmap words per receiver = key-list positions per pass / 64
 __host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw < BRC_WIDE_DCW ? nkw : BRC_WIDE_DCW; }
+// The consensus pass's deferred-SEND queue (brc_step.h, brc_life.h send_key): the SENDs one replica starts in
+// one step's pass -- one per phase end, consecutive phase indices -- at most SENDQ_MAX of them, else
+// BRC_OVERFLOW.  One bound for every kernel, so the step and key-lifetime kernels overflow at the same
+// point; 21 3-bit value ids fill a 64-bit queue word.  Measured with the oracle: at most 17 phase ends of
+// one replica in one step (cfg4, n = 64, round cap 64: bench.py's long leg, whose 2^20-instance GPU test sees
+// no overflow), 12 on the reference-pinned round-cap-64 fixture (tests/test_oracle_golden.py pins it).
+constexpr uint32_t SENDQ_MAX = 21;
 constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
 constexpr int KMODE_XREF = 4;               // ... reference protocol, sender peers, NPAD = 64 in the general
                                             // (non-lean) form: BRC_FLAG_GENERAL_KEYS

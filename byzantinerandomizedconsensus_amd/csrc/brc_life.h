@@ -258,8 +258,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     auto send_key = [&](uint32_t s, uint32_t v) {
         if (defer) {
             if (sq_n == 0) sq_s = s;
-            if (s == sq_s + sq_n && sq_n < 32u) { sq_v |= (uint64_t)(v & 3u) << (2 * sq_n); ++sq_n; }
-            else ovf = true;                             // cannot happen (consecutive indices, < 32 per step)
+            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v |= (uint64_t)(v & 3u) << (2 * sq_n); ++sq_n; }
+            else ovf = true;                             // consecutive indices; more than SENDQ_MAX in one step: overflow
             return;
         }
         send_key_now(s, v);
@@ -563,8 +563,12 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     // ring is an overflow, never lost; RW = 32: r <= 32 and delays <= 8 fit the 64 bits)
                     constexpr uint32_t DM1 = (1u << DL) - 1u;
                     if (PB && (r + hibit(x & DM1) > RW || r + hibit(x >> DL) > RW)) ovf = true;
-                    pendE |= (uint64_t)(x & DM1) << (r + 1u - PB);
-                    pendR |= (uint64_t)(x >> DL) << (r + 1u - PB);
+                    // a send at r = RW (RW = 64: a key past its 4 DLX-step lifetime bound) lands past the ring:
+                    // overflow above, and no shift by 64 (undefined; the hardware would wrap it to 0)
+                    if (r + 1u - PB < 64u) {
+                        pendE |= (uint64_t)(x & DM1) << (r + 1u - PB);
+                        pendR |= (uint64_t)(x >> DL) << (r + 1u - PB);
+                    }
                 }
             } else if (eb) {
                 if ((eb & Fm) && HF) pendE |= rb << 1;

@@ -783,7 +783,7 @@ void brc_step(const Params* __restrict__ pp) {
     auto send_key = [&](uint32_t s, uint32_t v) {
         if (defer_sends) {
             if (sq_n == 0) sq_s = s;
-            if (s == sq_s + sq_n && sq_n < 64u / VB) { sq_v |= (uint64_t)(v & VMASK) << (VB * sq_n); ++sq_n; }
+            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v |= (uint64_t)(v & VMASK) << (VB * sq_n); ++sq_n; }
             else ovf = true;                                 // cannot happen (consecutive indices, <= Q)
             return;
         }

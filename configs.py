@@ -17,8 +17,11 @@ Workloads:
   cfg4-conn-uniform[-d2]  connection peers under per-link uniform[1,4] ([1,2]) delays, 2^20
   cfg4-beb   the reference consensus over best-effort broadcast (BRC_MODE_BEB), 2^20
   cfg4-ref-r8  the reference protocol to round cap 8 (bench.py's many leg: the key-lifetime kernel), 2^20
+  cfg4-ref-r64, cfg4-spec-r64  SURVEY cfg4's round cap 64 (bench.py's long / spec64 legs), 2^20
   cfg4-conn-geometric  connection peers under geometric delays capped at 16 (64-row ring), 2^20
   cfg5-*     n=256 f=85 SPEC, 6144 instances per GPU, const / uniform[1,4] / geometric<=16
+  cfg5-conn-uniform  n=256 f=85, connection-identity peers (the reference as shipped), reference
+             protocol, uniform[1,4] delays, 6144 instances per GPU (the wide kernel's 40-B cells)
 
 A step is one pass of the hot path over the batch (reset + run to completion); the timed region
 is K steps between barriers, max over ranks.  `roofline.achieved` = this layout's algorithmic
@@ -76,9 +79,19 @@ def workloads(L):
     # the reference protocol to round cap 8 (bench.py's many leg; the key-lifetime kernel at 2^20)
     W["cfg4-ref-r8"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                             round_cap=8, key_window=32))
+    # SURVEY cfg4's round cap 64 (bench.py's long and spec64 legs): the reference protocol on the key-lifetime
+    # kernel (key window 128), SPEC on the step kernel (window 8), 2^20 each
+    W["cfg4-ref-r64"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                             round_cap=64, key_window=128))
+    W["cfg4-spec-r64"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
+                                              round_cap=64, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED))
     # connection peers under cfg5's geometric delays capped at 16 (the per-link form's 64-row ring)
     W["cfg4-conn-geometric"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=3, delay_max=16,
                                                     round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
+    # cfg5's committee with connection-identity peers (the reference as shipped, core/brbroadcast.py:69):
+    # the wide kernel's 40-B cells (the cell + two 16-step send-count rings), reference protocol, uniform[1,4]
+    W["cfg5-conn-uniform"] = (6144, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=1, delay_max=4,
+                                               round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
     for name, model, dmax in (("const", 0, 1), ("uniform", 1, 4), ("geometric", 3, 16)):
         # 6,144 instances per GPU: 8 waves of the 768 resident workgroups (3 per CU), so no partial last wave
         W["cfg5-" + name] = (6144, True, dict(base, n=256, f=85, seed=0x5EED0005, delay_model=model,
@@ -97,7 +110,7 @@ def cell_bytes(n, peer_mode=0):
 
 # configs.py workloads that are bench.py legs: their profiles are the bench's (workload "cfg4", mode = leg)
 BENCH_LEGS = {"cfg4-ref": "reference", "cfg4-spec": "spec", "cfg4-conn": "conn", "cfg4-conn-uniform-d2": "connu",
-              "cfg4-ref-r8": "many"}
+              "cfg4-ref-r8": "many", "cfg4-ref-r64": "long", "cfg4-spec-r64": "spec64"}
 
 
 def measured_profile(name, kernel_ms):
@@ -163,9 +176,14 @@ def roofline(name, n, bpc, cell_steps, kernel_ms, peer_mode=0, kernel="step"):
                "frac": None, "survey_model_gbs": bpc * cell_steps / sec / 1e9,
                "cell_steps_per_s": cell_steps / sec, "traffic": None, "traffic_frac": None,
                "note": "key-lifetime kernel: cells stay in registers for a key's lifetime, no HBM cell traffic "
-                       "(per-link form: one 8-B delivery-bitmap word per lane, key word and step in HBM); "
-                       "survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
-        return attach_profile(out, name, kernel_ms)
+                       "(per-link form: one 8-B delivery-bitmap word per lane, key word and step in HBM), so its "
+                       "roof is instruction issue: frac = max(VALU busy, SALU per CU-cycle) of the same-build "
+                       "profile (bench.py); survey_model_gbs prices SURVEY 8(d)'s %d B per cell-step at n=%d" % (bpc, n)}
+        out = attach_profile(out, name, kernel_ms)
+        if out.get("issue"):
+            out["frac"] = out["achieved"] = max(out["issue"]["valu_busy"], out["issue"]["salu_per_cu_cycle"])
+            out["unit"], out["peak"] = "issue-port fraction", 1.0
+        return out
     floor_b = 2 * cell_bytes(n, peer_mode)
     achieved = floor_b * cell_steps / sec / 1e9
     out = {"bound": "hbm", "kernel": "brc_step" if n <= 64 else "brc_step_wide", "unit": "GB/s", "peak": HBM_PEAK_GBS,

@@ -176,7 +176,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
 template <typename T> using gptr_t = __attribute__((address_space(1))) T*;
 template <typename T> __device__ __forceinline__ gptr_t<T> gp(T* p) { return (gptr_t<T>)p; }
 
-
 // one 24-B injection record through global (not flat) loads
 // the first 24 B of a record (everything but dst_hi, which only the wide kernel reads)
 __device__ __forceinline__ InjDev load_inj(const InjDev* p) {

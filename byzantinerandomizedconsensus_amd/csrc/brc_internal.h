@@ -43,10 +43,25 @@ __host__ __device__ inline uint32_t dpos_words_wide(uint32_t nkw) { return nkw <
 // The consensus pass's deferred-SEND queue (brc_step.h, brc_life.h send_key): the SENDs one replica starts in
 // one step's pass -- one per phase end, consecutive phase indices -- at most SENDQ_MAX of them, else
 // BRC_OVERFLOW.  One bound for every kernel, so the step and key-lifetime kernels overflow at the same
-// point; 21 3-bit value ids fill a 64-bit queue word.  Measured with the oracle: at most 17 phase ends of
+// point; the queue keeps 2-bit value ids in one 64-bit word, 3-bit ones one per nibble of two.  Measured with the oracle: at
+// most 17 phase ends of
 // one replica in one step (cfg4, n = 64, round cap 64: bench.py's long leg, whose 2^20-instance GPU test sees
-// no overflow), 12 on the reference-pinned round-cap-64 fixture (tests/test_oracle_golden.py pins it).
-constexpr uint32_t SENDQ_MAX = 21;
+// no overflow), 12 on the reference-pinned round-cap-64 fixture (tests/test_oracle_golden.py pins it); with
+// every link at delay 1 up to 27 (tests/test_gpu_life.py ref-const64-cap30-q32).
+constexpr uint32_t SENDQ_MAX = 32;
+template <uint32_t VB> struct SendQ {      // the queued SENDs' VB-bit value ids (VB = 3: entry i in nibble i % 16 of word i / 16)
+    uint64_t w[VB == 2 ? 1 : 2];
+    __device__ __forceinline__ void clear() { for (auto& x : w) x = 0; }
+    __device__ __forceinline__ void put(uint32_t i, uint32_t v) {
+        if constexpr (VB == 2) { w[0] |= (uint64_t)(v & 3u) << (2 * i); return; }
+        const uint64_t x = (uint64_t)(v & 15u) << (4 * (i & 15u));
+        if (i < 16) w[0] |= x; else w[VB == 2 ? 0 : 1] |= x;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        if constexpr (VB == 2) return (uint32_t)(w[0] >> (2 * i)) & 3u;
+        return (uint32_t)((i < 16 ? w[0] : w[VB == 2 ? 0 : 1]) >> (4 * (i & 15u))) & 15u;
+    }
+};
 constexpr int KMODE_CONN = 3;               // kernel mode: reference protocol, connection-identity peers
 constexpr int KMODE_XREF = 4;               // ... reference protocol, sender peers, NPAD = 64 in the general
                                             // (non-lean) form: BRC_FLAG_GENERAL_KEYS

@@ -254,19 +254,20 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // of one pass have consecutive phase indices: the first index and a 2-bit value each.
     bool defer = false;
     uint32_t sq_s = 0, sq_n = 0;
-    uint64_t sq_v = 0;
+    SendQ<2> sq_v;
+    sq_v.clear();
     auto send_key = [&](uint32_t s, uint32_t v) {
         if (defer) {
             if (sq_n == 0) sq_s = s;
-            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v |= (uint64_t)(v & 3u) << (2 * sq_n); ++sq_n; }
+            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v.put(sq_n, v & 3u); ++sq_n; }
             else ovf = true;                             // consecutive indices; more than SENDQ_MAX in one step: overflow
             return;
         }
         send_key_now(s, v);
     };
     auto flush_sends = [&]() {
-        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (2 * i)) & 3u);
-        sq_n = 0; sq_v = 0;
+        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, sq_v.get(i) & 3u);
+        sq_n = 0; sq_v.clear();
     };
     // a slot's consensus view: value << 14 | (s + 1), as the BRB phase left it
     // (HM: the consensus passes read it from their s_sv snapshot of the word being consumed, snap_w)

@@ -778,19 +778,20 @@ void brc_step(const Params* __restrict__ pp) {
     // the index by one): the queue keeps the first index and a VB-bit value id per SEND.
     bool defer_sends = false;
     uint32_t sq_s = 0, sq_n = 0;
-    uint64_t sq_v = 0;
+    SendQ<VB> sq_v;
+    sq_v.clear();
     auto send_key = [&](uint32_t s, uint32_t v) {
         if (defer_sends) {
             if (sq_n == 0) sq_s = s;
-            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v |= (uint64_t)(v & VMASK) << (VB * sq_n); ++sq_n; }
-            else ovf = true;                                 // cannot happen (consecutive indices, <= Q)
+            if (s == sq_s + sq_n && sq_n < SENDQ_MAX) { sq_v.put(sq_n, v & VMASK); ++sq_n; }
+            else ovf = true;                                 // consecutive indices; past SENDQ_MAX: overflow
             return;
         }
         send_key_now(s, v);
     };
     auto flush_sends = [&]() {
-        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, (uint32_t)(sq_v >> (VB * i)) & VMASK);
-        sq_n = 0; sq_v = 0;
+        for (uint32_t i = 0; i < sq_n; ++i) send_key_now(sq_s + i, sq_v.get(i) & VMASK);
+        sq_n = 0; sq_v.clear();
     };
     auto get_max_val = [&](uint32_t bound2) -> uint32_t {          // :64-68
         for (uint32_t i = 0; i < nvals; ++i) {

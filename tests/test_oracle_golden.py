@@ -57,7 +57,7 @@ def test_fixture_inventory():
 def test_phase_ends_per_step_within_the_send_queue_bound():
     """The engine queues the SENDs one replica starts in one step's consensus pass (one per phase end:
     the reference's phase leakage, core/byzantinerandomizedconsensus.py:57-61, :71-78, lets a replica end
-    several phases in one step) and reports BRC_OVERFLOW past SENDQ_MAX = 21 (csrc/brc_internal.h; every
+    several phases in one step) and reports BRC_OVERFLOW past SENDQ_MAX = 32 (csrc/brc_internal.h; every
     kernel has this one bound).  On the reference-pinned many-round fixtures -- round caps 8 and 64 --
     the oracle's largest count of SENDs by one replica in one step stays below it (12; cfg4's round cap
     64 at n = 64 reaches 17, and its 2^20-instance GPU test, test_cfg4_round_cap_64_2p20_bench_legs,
@@ -69,4 +69,4 @@ def test_phase_ends_per_step_within_the_send_queue_bound():
             got = oracle.run(case["spec"], kinds=("send",))
             per = collections.Counter((t, node) for (t, node, typ, _kp, _s) in got["events"]["send"] if typ == 1)
             worst = max(worst, max(per.values()))
-    assert 1 < worst <= 21, worst
+    assert 1 < worst <= 32, worst

@@ -518,7 +518,7 @@ int brc_create(const brc_config* cfg, void** out) {
         {(void**)&e->dparams, sizeof(Params)},
         {(void**)&e->dbits, (e->compact && spec && e->step_ok) ? (size_t)e->nitems * e->nkw * 64 * 8 : 8},
         {(void**)&e->dring, (e->life_cfg && e->life_pl) ? (size_t)e->nitems * e->life_rw * e->nkw * 64 * 8 : 8},
-        {(void**)&e->lmeta, (e->life_cfg && life_hbm_meta(c.key_window, e->life_pl)) ? (size_t)e->nitems * e->NK * 4 : 8},
+        {(void**)&e->lmeta, (e->life_cfg && life_hbm_meta(c.key_window, e->life_pl)) ? (size_t)e->nitems * e->NK * 8 : 8},
         // extra-SEND records: the non-lean narrow kernels only (the lean and wide kernels refuse extra SENDs)
         {(void**)&e->xsend, (e->compact || e->wide) ? 8 : (size_t)e->nitems * XSEND_MAX * 24},
         {(void**)&e->xsn, (e->compact || e->wide) ? 8 : (size_t)e->nitems * 4},

@@ -125,7 +125,8 @@ struct Params {
     brc_event* events; unsigned long long* event_count;
     uint64_t* dbits;              // lean SPEC: per-wave delivery bitmaps [item][nkw][64] (brc_step.h DBG)
     uint64_t* dring;              // per-link key-lifetime kernel: delivery bitmap ring [item][LIFE_RW or LIFE_RW16][nkw][64] (brc_life.h)
-    uint32_t* lmeta;              // key-lifetime kernel, key windows >= 64: key-slot metadata [item][NK] in HBM (brc_life.h)
+    uint32_t* lmeta;              // key-lifetime kernel, key windows >= 32: key-slot metadata + class delivery steps
+                                  // [item][2][NK] u32 in HBM (brc_life.h)
     uint64_t* xsend;              // non-lean step kernels: extra-SEND records [item][XSEND_MAX][3] (brc_step.h)
     uint32_t* xsn;                // ... records in use per item
     unsigned long long* gcount;   // [0] cell_steps [1] arrivals [2] msgs [3] deliveries [4] lane loads [5] max s
@@ -243,9 +244,13 @@ constexpr uint32_t LIFE_RW = 32;
 #define BRC_LIFE_HM_Q 32
 #endif
 __host__ __device__ inline bool life_hbm_meta(uint32_t Q, bool perlink) { return !perlink && Q >= BRC_LIFE_HM_Q; }
+// Their class delivery steps live in HBM too (one u32 per slot beside the metadata: 8 B per slot in
+// P.lmeta); LDS keeps, per ring step, the key words with a delivery then (LIFE_RW rows x 128 bits) and the
+// consumed words' class bitmaps (16 B per key word).
 __host__ __device__ inline uint32_t lds_bytes_life(uint32_t NK, bool spec, uint32_t Q, uint32_t nv, bool perlink) {
-    const uint32_t meta = life_hbm_meta(Q, perlink) ? 4u * 128u : 4u * NK;
-    return ((meta + (perlink ? 0u : 2 * NK) + 7) & ~7u) + 8 * cons_words(spec, 8, Q, nv);
+    if (life_hbm_meta(Q, perlink))
+        return 4u * 128u + 16u * 32u + 16u * ((NK + 63) / 64) + 8 * cons_words(spec, 8, Q, nv);
+    return ((4u * NK + (perlink ? 0u : 2 * NK) + 7) & ~7u) + 8 * cons_words(spec, 8, Q, nv);
 }
 // Launch the key-lifetime kernel (brc_kern_life.hip): one 64-lane workgroup per instance
 // (perlink: uniform / geometric delays, delivery bitmaps in P.dring; dm16: delays up to 16, whose

@@ -92,18 +92,26 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // s_sv), against a lifetime of ~20 simulated steps
     constexpr bool HM = QBIG || HMT;
     static_assert(!(HM && PL), "HBM slot metadata: two-class form");
-    uint32_t* const g_meta = HM ? P.lmeta + item * (uint64_t)NK : nullptr;
+    uint32_t* const g_meta = HM ? P.lmeta + item * (uint64_t)NK * 2 : nullptr;
+    // HM: the class delivery steps too (below), one u32 per slot: class A's code | class B's << 8, written
+    // whole when the key is simulated (a reused slot's old key is quiet, its deliveries all consumed)
+    uint32_t* const g_dab = HM ? g_meta + NK : nullptr;
     uint32_t* s_meta = (uint32_t*)smem;
     uint32_t* s_sv = (uint32_t*)smem;             // HM: metadata snapshot of the key words being consumed [2][64]
+    // HM: per ring step (t mod LIFE_RW) the key words with a class delivery then ([32][2] u64, bit w), and the
+    // step's consumed class bitmaps of those words ([nkw][2] u64: class A, class B)
+    uint64_t* const s_wsum = (uint64_t*)smem + 64;
+    uint64_t* const s_kab = (uint64_t*)smem + 128;
     // two-class form: the step at which each receiver class delivers key slot k -- a class's honest
     // receivers evolve identically, so a class delivers a key once, at one step, whole.  One byte,
     // 0x80 | step mod 128 (0: none): a key's deliveries lie within 4 Dd <= 32 steps of its creation, and
     // the consensus pass clears the entries of the step it consumes (every entry's step is one it visits:
     // a delivery lands on an honest class, so its step has arrivals), so no stale entry aliases a later
     // step.  The per-link form keeps its deliveries in HBM (P.dring).
-    uint8_t* s_dA = (uint8_t*)(s_meta + (HM ? 128u : NK));   // (PL: unused)
+    uint8_t* s_dA = (uint8_t*)(s_meta + NK);     // (PL, HM: unused)
     uint8_t* s_dB = s_dA + NK;
-    uint64_t* s_hm = (uint64_t*)((char*)smem + ((4 * (HM ? 128u : NK) + (PL ? 0u : 2 * NK) + 7) & ~7u));   // REFERENCE / BEB: hosts per value [4][64]
+    uint64_t* s_hm = HM ? s_kab + 2 * nkw                                   // REFERENCE / BEB: hosts per value [4][64]
+                        : (uint64_t*)((char*)smem + ((4 * NK + (PL ? 0u : 2 * NK) + 7) & ~7u));
     // slot metadata word k: LDS, or (HM) this instance's HBM row through agent-scope relaxed atomics (L2-served,
     // in program order for one location, as the delivery ring P.dring is accessed)
     auto mld = [&](uint32_t k) -> uint32_t {
@@ -194,8 +202,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // ---- LDS init
     for (uint32_t i = lane; i < NK; i += 64) {
         mst(i, 0u);
-        if (!PL) { s_dA[i] = 0; s_dB[i] = 0; }
+        if (HM) __hip_atomic_store(g_dab + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else if (!PL) { s_dA[i] = 0; s_dB[i] = 0; }
     }
+    if (HM) s_wsum[lane] = 0;
     if constexpr (SPEC) {
         for (uint32_t q = 0; q < Q; ++q) {
             if (seen_on) s_seen[q * 64 + lane] = 0;
@@ -376,6 +386,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         Ring16 ringR = {0ull, 0ull};                  // PL connection peers: READY copies per step
         uint32_t last = t0;
         uint32_t prv = 0;                             // CONN two-class: READY copies landing at relative step = lane
+        uint32_t dab = 0;                             // HM: the key's class delivery codes (A | B << 8)
         const uint32_t kw = k >> 6;
         const uint64_t kbit = 1ull << (k & 63);
         for (uint64_t pend = pendS; pend; pend = pendS | pendE | pendR) {
@@ -545,8 +556,13 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 // receivers of one class evolve identically: a delivery step takes whole honest classes
                 const uint64_t dA = db & HF, dB = db & HS;
                 if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
-                if (dA && lane == 0) s_dA[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
-                if (dB && lane == 0) s_dB[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
+                if constexpr (HM) {
+                    dab |= (dA ? (0x80u | (ts & 0x7Fu)) : 0u) | (dB ? (0x80u | (ts & 0x7Fu)) << 8 : 0u);
+                    if (lane == 0) s_wsum[row * 2 + (kw >> 6)] |= 1ull << (kw & 63);   // a delivery of word kw at ts
+                } else {
+                    if (dA && lane == 0) s_dA[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
+                    if (dB && lane == 0) s_dB[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
+                }
             }
             // the messages sent now land on fast receivers after 1 step (fast senders) and on every
             // other (sender, receiver) pair after Dd steps
@@ -592,7 +608,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             rows |= (RowT)1 << row;
             last = ts;
         }
-        if (lane == 0) mst(k, (mld(k) & 0xFFFFu) | (last << 16));
+        if (lane == 0) {
+            mst(k, (mld(k) & 0xFFFFu) | (last << 16));
+            if (HM) __hip_atomic_store(g_dab + k, dab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     };
     // the keys created this step (every lane's clr_s .. clr_s + clr_n - 1), each simulated once
     auto simulate_new = [&]() {
@@ -655,6 +674,41 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         }
         // ================= consensus: this step's deliveries in canonical (kp, s) order
         defer = true;
+        // HM: the key words the step's summary row flags -- their class codes read from HBM 8 words at a time,
+        // consumed entries cleared, the two class bitmaps of each kept in LDS for dword()
+        uint64_t fw[2] = {0ull, 0ull};
+        if constexpr (HM) {
+            const uint32_t tc = 0x80u | (t & 0x7Fu);
+            fw[0] = uni64(s_wsum[row * 2]); fw[1] = uni64(s_wsum[row * 2 + 1]);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane < 2) s_wsum[row * 2 + lane] = 0;       // consumed: the row is free for step t + LIFE_RW
+            uint64_t pend[2] = {fw[0], fw[1]};
+#pragma unroll 1
+            while (pend[0] | pend[1]) {
+                uint32_t wl[8], x[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int h = pend[0] ? 0 : 1;
+                    wl[i] = 0xFFFFFFFFu; x[i] = 0u;
+                    if (pend[h]) {
+                        wl[i] = 64u * (uint32_t)h + (uint32_t)__builtin_ctzll(pend[h]);
+                        pend[h] &= pend[h] - 1;
+                        x[i] = __hip_atomic_load(g_dab + wl[i] * 64 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    if (wl[i] == 0xFFFFFFFFu) continue;
+                    const bool a = (x[i] & 0xFFu) == tc, b = ((x[i] >> 8) & 0xFFu) == tc;
+                    const uint64_t kA = __ballot(a), kB = __ballot(b);
+                    if (lane == 0) { s_kab[2 * wl[i]] = kA; s_kab[2 * wl[i] + 1] = kB; }
+                    if (a || b)                              // consumed: free the entries for step t + 128
+                        __hip_atomic_store(g_dab + wl[i] * 64 + lane, x[i] & ~((a ? 0xFFu : 0u) | (b ? 0xFF00u : 0u)),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
         // this step's delivery bits of key word w for this lane (read once: PL clears the ring word)
         auto dword = [&](uint32_t w) -> uint64_t {
             uint64_t bits;
@@ -663,6 +717,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 bits = __hip_atomic_load(dp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (bits) __hip_atomic_store(dp, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (!cons_lane) bits = 0;
+            } else if constexpr (HM) {
+                bits = 0;
+                if (cons_lane && ((fw[w >> 6] >> (w & 63)) & 1ull)) bits = s_kab[2 * w + (laneF ? 0u : 1u)];
             } else {
                 // the keys of word w whose delivery step for this lane's class is now
                 const uint32_t kk = w * 64 + lane, tc = 0x80u | (t & 0x7Fu);

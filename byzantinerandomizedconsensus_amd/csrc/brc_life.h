@@ -558,7 +558,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 if ((dA && dA != HF) || (dB && dB != HS)) ovf = true;
                 if constexpr (HM) {
                     dab |= (dA ? (0x80u | (ts & 0x7Fu)) : 0u) | (dB ? (0x80u | (ts & 0x7Fu)) << 8 : 0u);
-                    if (lane == 0) s_wsum[row * 2 + (kw >> 6)] |= 1ull << (kw & 63);   // a delivery of word kw at ts
+                    if (lane == 0)                           // a delivery of word kw at ts (no-return LDS OR: no wait)
+                        atomicOr((unsigned long long*)&s_wsum[row * 2 + (kw >> 6)], 1ull << (kw & 63));
                 } else {
                     if (dA && lane == 0) s_dA[k] = (uint8_t)(0x80u | (ts & 0x7Fu));
                     if (dB && lane == 0) s_dB[k] = (uint8_t)(0x80u | (ts & 0x7Fu));

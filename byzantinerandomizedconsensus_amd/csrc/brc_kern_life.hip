@@ -36,3 +36,12 @@ int launch_life(int mode, bool perlink, bool dm16, bool qbig, bool hm, uint32_t 
     return perlink ? launch_life_pl<true, 8>(mode, blocks, lds, s, P) : launch_life_pl<false, 8>(mode, blocks, lds, s, P);
 }
 }  // namespace brc
+
+#ifdef BRC_STAMPS
+// dev-only: the lifetime kernel's section timers (tools/stamps.py)
+extern "C" int brc_dbg_stamps_life(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(brc::brc_stamps), BRC_NSTAMPS * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[BRC_NSTAMPS] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(brc::brc_stamps), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

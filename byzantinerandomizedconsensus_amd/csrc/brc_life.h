@@ -657,6 +657,15 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     else simulate_new();
 
     const uint64_t gm0 = (Q >= 64) ? ~0ull : ((1ull << Q) - 1);
+#ifdef BRC_STAMPS
+    // dev-only section timers (tools/stamps.py life): step head, HM class-code reads, consensus words,
+    // sends + stop checks, lifetime simulation of the new keys
+    uint64_t stamp_acc[5] = {0, 0, 0, 0, 0};
+    uint64_t stamp_prev = __builtin_amdgcn_s_memtime();
+#define LIFE_STAMP(i) do { const uint64_t _n = __builtin_amdgcn_s_memtime(); stamp_acc[i] += _n - stamp_prev; stamp_prev = _n; } while (0)
+#else
+#define LIFE_STAMP(i) do {} while (0)
+#endif
     while (status == BRC_RUNNING) {
         // next step with arrivals at an honest receiver
         const uint32_t rot = (t + 1) & (RW - 1);
@@ -675,6 +684,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         }
         // ================= consensus: this step's deliveries in canonical (kp, s) order
         defer = true;
+        LIFE_STAMP(0);
         // HM: the key words the step's summary row flags -- their class codes read from HBM 8 words at a time,
         // consumed entries cleared, the two class bitmaps of each kept in LDS for dword()
         uint64_t fw[2] = {0ull, 0ull};
@@ -710,6 +720,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
+        LIFE_STAMP(1);
         // this step's delivery bits of key word w for this lane (read once: PL clears the ring word)
         auto dword = [&](uint32_t w) -> uint64_t {
             uint64_t bits;
@@ -849,6 +860,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        LIFE_STAMP(2);
         defer = false;
         flush_sends();                                // the SENDs this step's consensus started
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -861,9 +873,15 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         const uint64_t b_und = __ballot(honest && dcount < P.round_cap);
         if (__ballot(ovf)) status = BRC_OVERFLOW;
         else if (P.round_cap > 0 && !b_und) status = BRC_DONE;
-        else simulate_new();                          // the keys this step's consensus created
+        LIFE_STAMP(3);
+        if (status == BRC_RUNNING) simulate_new();    // the keys this step's consensus created
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        LIFE_STAMP(4);
     }
+#ifdef BRC_STAMPS
+    if (lane == 0) for (int i = 0; i < 5; ++i) atomicAdd(&brc_stamps[i], (unsigned long long)stamp_acc[i]);
+#endif
+#undef LIFE_STAMP
     if (__ballot(ovf) && status != BRC_OVERFLOW) status = BRC_OVERFLOW;
     if constexpr (PL) {
         // rows of steps the instance did not reach: leave the bitmap ring zero for the next launch

@@ -56,6 +56,12 @@ constexpr uint32_t LIFE_NEVER = 0xFFFFu;         // relative send step: not sent
 __device__ __forceinline__ uint32_t lm_s1(uint32_t m) { return m & 0x3FFFu; }
 __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 
+#ifndef BRC_LIFE_LANES
+#define BRC_LIFE_LANES 1   // two-class form, sender peers: the new keys' lifetimes simulated one key per lane
+#endif
+#ifndef BRC_LIFE_LANES_WAVES
+#define BRC_LIFE_LANES_WAVES 8   // their waves per SIMD
+#endif
 #ifndef BRC_LIFE_PL_CONN_WAVES
 #define BRC_LIFE_PL_CONN_WAVES 6   // per-link form, connection peers: waves per SIMD (A/B: 5 284.4, 6 273.2, 7 277.5 ms)
 #endif
@@ -65,7 +71,7 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 // are instantiations of their own, so the default ones keep their registers.
 // HMT: the slot metadata in HBM (key windows >= 32, two-class form; QBIG implies it)
 template <int MODE, bool PL, int DLX = 8, bool QBIG = false, bool HMT = false>
-__global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAVES : 6) : 8) void brc_life(const Params* __restrict__ pp) {
+__global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAVES : 6) : (MODE != KMODE_CONN && BRC_LIFE_LANES) ? BRC_LIFE_LANES_WAVES : 8) void brc_life(const Params* __restrict__ pp) {
     const Params& P = *pp;
     constexpr bool SPEC = MODE == BRC_MODE_SPEC, BEB = MODE == BRC_MODE_BEB, CONN = MODE == KMODE_CONN;
     static_assert(DLX == 8 || (PL && DLX == 16), "delays up to 16: per-link form");
@@ -360,6 +366,59 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         spec_advance();
     };
 
+    // the BRB cell handler of one receiver at one relative step, sender-identity peers (core/brbroadcast.py:60-119;
+    // brc_step.h process_pair): opn = the cell is open and has arrivals, sa / ea / ra its SEND / ECHO / READY
+    // arrivals, hS / hE / hR the key's message types landing now; es / rs / dl: ECHO / READY sent, delivered
+    auto upd_cell = [&](uint32_t& fl, uint32_t& ec, uint32_t& rc, bool opn, uint32_t sa, uint32_t ea, uint32_t ra,
+                        bool hS, bool hE, bool hR, uint32_t& es, uint32_t& rs, uint32_t& dl) {
+        auto ge = [](uint32_t x, uint32_t y) -> uint32_t { return ((x - y) >> 31) ^ 1u; };   // x >= y (< 2^31)
+        if constexpr (BEB) {
+            dl = (opn && sa) ? 1u : 0u;                             // brb_cell_update_beb
+            fl |= dl << 2;
+        } else if constexpr (SPEC) {
+            if (hS) { es = (opn ? sa : 0u) & ~(fl >> 3) & 1u; fl |= es << 3; }   // brb_cell_update_spec
+            if (hE || hR) {
+                ec += opn ? ea : 0u;
+                rc += opn ? ra : 0u;
+                rs = (opn ? 1u : 0u) & ~(fl >> 4) & (ge(ec, T_echo) | ge(rc, T_amp));
+                fl |= rs << 4;
+                dl = (opn ? 1u : 0u) & ge(rc, T_del);
+                fl |= dl << 2;
+            }
+        } else {
+            // brb_cell_update in integer form (brc_step.h process_pair).  F_EEX = bit 0, F_REX = 1,
+            // F_DEL = 2, F_ES = 3, F_RS = 4.
+            if (hS) {                                                // :76-82
+                es = (opn ? sa : 0u) & ~fl & 1u;
+                fl |= es | (es << 3);
+            }
+            if (hE) {                                                // :84-98
+                const uint32_t e = opn ? ea : 0u;
+                const uint32_t eon = min(e, 1u);
+                const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
+                fl |= eon;
+                ec += e;
+                const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
+                fl |= (r1 << 1) | (r1 << 4);
+                rs = r1;
+            }
+            if (hR) {                                                // :100-119
+                const uint32_t x = opn ? ra : 0u;
+                const uint32_t ron = min(x, 1u);
+                const uint32_t rexm = 0u - ((fl >> 1) & 1u);
+                const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
+                fl |= ron << 1;
+                rc += x;
+                const uint32_t any = ron & ge(rhi, rlo);
+                const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+                const uint32_t r2 = any & ~fl & ~(fl >> 4) & ge(ahi, alo) & 1u;
+                fl |= r2 << 4;
+                dl = any & ge(rhi, T_del);
+                fl |= dl << 2;
+                rs |= r2;
+            }
+        }
+    };
     // ---- the lifetime of key slot k created at step t (wave-uniform): every step at which one of
     // its messages lands on an honest receiver, in order; cells in registers (brc_step.h C32 fields
     // unpacked: flags, |echo set|, |ready set|, and the relative steps this lane SENT ECHO / READY)
@@ -488,51 +547,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 fl |= dl << 2;
                 rs = min(nr, 1u);
                 fl |= rs << 4;
-            } else if constexpr (BEB) {
-                dl = (opn && sa) ? 1u : 0u;                             // brb_cell_update_beb
-                fl |= dl << 2;
-            } else if constexpr (SPEC) {
-                if (hS) { es = (opn ? sa : 0u) & ~(fl >> 3) & 1u; fl |= es << 3; }   // brb_cell_update_spec
-                if (hE || hR) {
-                    ec += opn ? ea : 0u;
-                    rc += opn ? ra : 0u;
-                    rs = (opn ? 1u : 0u) & ~(fl >> 4) & (ge(ec, T_echo) | ge(rc, T_amp));
-                    fl |= rs << 4;
-                    dl = (opn ? 1u : 0u) & ge(rc, T_del);
-                    fl |= dl << 2;
-                }
             } else {
-                // brb_cell_update in integer form (brc_step.h process_pair).  F_EEX = bit 0, F_REX = 1,
-                // F_DEL = 2, F_ES = 3, F_RS = 4.
-                if (hS) {                                                // :76-82
-                    es = (opn ? sa : 0u) & ~fl & 1u;
-                    fl |= es | (es << 3);
-                }
-                if (hE) {                                                // :84-98
-                    const uint32_t e = opn ? ea : 0u;
-                    const uint32_t eon = min(e, 1u);
-                    const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
-                    fl |= eon;
-                    ec += e;
-                    const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
-                    fl |= (r1 << 1) | (r1 << 4);
-                    rs = r1;
-                }
-                if (hR) {                                                // :100-119
-                    const uint32_t x = opn ? ra : 0u;
-                    const uint32_t ron = min(x, 1u);
-                    const uint32_t rexm = 0u - ((fl >> 1) & 1u);
-                    const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
-                    fl |= ron << 1;
-                    rc += x;
-                    const uint32_t any = ron & ge(rhi, rlo);
-                    const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
-                    const uint32_t r2 = any & ~fl & ~(fl >> 4) & ge(ahi, alo) & 1u;
-                    fl |= r2 << 4;
-                    dl = any & ge(rhi, T_del);
-                    fl |= dl << 2;
-                    rs |= r2;
-                }
+                upd_cell(fl, ec, rc, opn, sa, ea, ra, hS, hE, hR, es, rs, dl);
             }
             const uint64_t eb = __ballot(es != 0), rbm = __ballot(rs != 0), db = __ballot(dl != 0);
             if (es) rE = r;
@@ -614,8 +630,137 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             if (HM) __hip_atomic_store(g_dab + k, dab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     };
+    // ---- two-class form, sender peers (LANES): the keys created this step simulated one per lane -- lane L
+    // takes one key of origin L (a batch per key index of each origin).  A key's honest receivers of one
+    // class evolve identically (above), so its lifetime is two class states, A (honest fast receivers) and
+    // B (honest slow ones), advanced by upd_cell per relative step r; a class's arrival count is a
+    // comparison of the class states' send steps times the class sizes (simulate()'s ballot popcounts in
+    // closed form), and the step statistics are wave sums over the batch.  The keys are independent, so
+    // this is simulate(k) for every key of the batch at once: the same slot stamps, class delivery steps,
+    // ring statistics and overflows, in VALU instead of the scalar unit, which simulate() saturates.
+    constexpr bool LANES = BRC_LIFE_LANES && !PL && !CONN;
+    auto simulate_batch = [&](const bool has, const uint32_t k) {
+        const bool vA = HF != 0, vB = HS != 0;
+        const bool oF = laneF;                        // the origin is this lane
+        const uint32_t sdlA = oF ? 1u : Dd;           // SEND arrival step at class A (class B: Dd)
+        // pending message types of the next steps, a window sliding with r: bit j of field S (bits 0-9),
+        // E (10-19), R (20-29) <=> step r + j (a message lands at most Dd <= 8 steps after it is sent)
+        uint32_t pend = 0;
+        if (has) {
+            if (oF && vA) pend |= 1u;
+            if (vB || (!oF && vA)) pend |= 1u << (Dd - 1u);
+        }
+        uint32_t flA = 0, ecA = 0, rcA = 0, flB = 0, ecB = 0, rcB = 0;
+        // the relative steps the classes SENT ECHO / READY, a byte each (0xFF: not sent): A's ECHO, A's READY,
+        // B's ECHO, B's READY
+        uint32_t sent = 0xFFFFFFFFu;
+        uint32_t last = t, dab = 0;
+        const uint32_t kw = k >> 6;
+#pragma unroll 1
+        for (uint32_t r = 1; ; ++r) {
+            if (!__ballot(pend != 0u)) break;
+            const bool hS = (pend & 1u) != 0, hE = (pend & (1u << 10)) != 0, hR = (pend & (1u << 20)) != 0;
+            bool act = hS || hE || hR;
+            if (act && r > RW) {                      // past the ring: overflow (cannot happen for Dd <= 8)
+                ovf = true; act = false;
+                pend = 0;
+            }
+            const uint32_t ts = t + r, row = ts & (RW - 1);
+            const uint32_t c1 = r - 1u, cD = r >= Dd ? r - Dd : 0x100u;   // 0x100: matches no byte
+            // class arrivals: fast senders (class A) land on A after 1 step, every other pair after Dd
+            uint32_t eA = 0, eB = 0, rA = 0, rB = 0;
+            if (hE) {
+                const uint32_t xA = sent & 0xFFu, xB = (sent >> 16) & 0xFFu;
+                eA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                eB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+            }
+            if (hR) {
+                const uint32_t xA = (sent >> 8) & 0xFFu, xB = sent >> 24;
+                rA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                rB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+            }
+            const uint32_t saA = (hS && r == sdlA) ? 1u : 0u, saB = (hS && r == Dd) ? 1u : 0u;
+            const uint32_t aA = act ? eA + rA + saA : 0u, aB = act ? eB + rB + saB : 0u;
+            // a delivered cell ignores everything (core/brbroadcast.py:74)
+            const bool opnA = vA && aA != 0 && !(flA & F_DEL), opnB = vB && aB != 0 && !(flB & F_DEL);
+            uint32_t esA = 0, rsA = 0, dlA = 0, esB = 0, rsB = 0, dlB = 0;
+            if (act) {
+                upd_cell(flA, ecA, rcA, opnA, saA, eA, rA, hS, hE, hR, esA, rsA, dlA);
+                upd_cell(flB, ecB, rcB, opnB, saB, eB, rB, hS, hE, hR, esB, rsB, dlB);
+            }
+            if (esA | rsA | esB | rsB) {
+                const uint32_t sm = (esA ? 0xFFu : 0u) | (rsA ? 0xFF00u : 0u) | (esB ? 0xFF0000u : 0u) | (rsB ? 0xFF000000u : 0u);
+                sent = (sent & ~sm) | ((r * 0x01010101u) & sm);
+            }
+            // step statistics over the batch: arrivals nHF aA + nHS aB, messages n (nHF (esA + rsA) + nHS (esB +
+            // rsB)), cells nHF [aA > 0] + nHS [aB > 0], deliveries nHF dlA + nHS dlB (simulate()'s popcounts)
+            const uint64_t am = __ballot(act);
+            if (am) {
+                const uint32_t s1 = wave_sum(aA | (aB << 16));
+                const uint32_t s2 = wave_sum((esA + rsA) | ((esB + rsB) << 8) | ((aA != 0 ? 1u : 0u) << 16) |
+                                             ((aB != 0 ? 1u : 0u) << 24));
+                const uint32_t ndA = (uint32_t)__popcll(__ballot(dlA != 0)), ndB = (uint32_t)__popcll(__ballot(dlB != 0));
+                const uint32_t arr = nHF * (s1 & 0xFFFFu) + nHS * (s1 >> 16);
+                const uint32_t msgs = n * (nHF * (s2 & 0xFFu) + nHS * ((s2 >> 8) & 0xFFu));
+                const uint32_t cells = nHF * ((s2 >> 16) & 0xFFu) + nHS * (s2 >> 24);
+                const uint32_t dels = nHF * ndA + nHS * ndB;
+                const bool mine = lane == row;
+                rg_arr += mine ? arr : 0u; rg_msg += mine ? msgs : 0u;
+                rg_cell += mine ? cells : 0u; rg_del += mine ? dels : 0u;
+                acc_add(4u, (uint32_t)__popcll(am));
+                rows |= (RowT)1 << row;
+            }
+            if (dlA || dlB) {
+                // a class delivers the key at step ts, whole
+                const uint32_t tc = 0x80u | (ts & 0x7Fu);
+                if constexpr (HM) {
+                    dab |= (dlA ? tc : 0u) | (dlB ? tc << 8 : 0u);
+                    // a delivery of word kw at ts (no-return LDS OR)
+                    atomicOr((unsigned long long*)&s_wsum[row * 2 + (kw >> 6)], 1ull << (kw & 63));
+                } else {
+                    if (dlA) s_dA[k] = (uint8_t)tc;
+                    if (dlB) s_dB[k] = (uint8_t)tc;
+                }
+            }
+            // the messages sent now land on class A after 1 step (fast senders) and on every other pair
+            // after Dd steps
+            if (esA || esB) {
+                if (esA) pend |= 1u << 11;
+                if (vB || esB) pend |= 1u << (10u + Dd);
+            }
+            if (rsA || rsB) {
+                if (rsA) pend |= 1u << 21;
+                if (vB || rsB) pend |= 1u << (20u + Dd);
+            }
+            if (act) last = ts;
+            pend = (pend >> 1) & ~((1u << 9) | (1u << 19));   // step r consumed: the window moves to r + 1
+        }
+        if (has) {
+            mst(k, (mld(k) & 0xFFFFu) | (last << 16));
+            if (HM) __hip_atomic_store(g_dab + k, dab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     // the keys created this step (every lane's clr_s .. clr_s + clr_n - 1), each simulated once
     auto simulate_new = [&]() {
+        if constexpr (LANES) {
+#pragma unroll 1
+            for (;;) {
+                bool has;
+                uint32_t k = 0;
+                if constexpr (QBIG) {
+                    has = clr_n != 0;
+                    if (has) { k = (lane * NV) * Q + (clr_s & Qm); ++clr_s; --clr_n; }
+                } else {
+                    has = clr != 0;
+                    if (has) { k = (lane * NV) * Q + (uint32_t)__ffs(clr) - 1u; clr &= clr - 1u; }
+                }
+                if (!__ballot(has)) break;
+                simulate_batch(has, k);
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            }
+            clr = 0; clr_n = 0;
+            return;
+        }
         if constexpr (QBIG) {
             for (uint64_t b = __ballot(clr_n != 0); b; b &= b - 1) {
                 const int L = __ffsll((unsigned long long)b) - 1;

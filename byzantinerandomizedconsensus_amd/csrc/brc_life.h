@@ -17,11 +17,13 @@
 //
 // Two-class delays.  Under the constant and slow-set models a link's delay
 // is 1 when both ends are "fast" and Dd otherwise (constant: no fast class, Dd = the constant).
-// Every receiver of a class therefore sees the same arrival counts; they are computed once per
-// class with scalar popcounts of the senders' ballots (two per message type) and selected per
-// lane.  The per-receiver cell update still runs on every lane.  Receivers of one class evolve
-// identically, so a key's deliveries at a step are whole honest classes; the consensus pass
-// reads them as two per-class key bitmaps per step.  A key's messages all land within 4 Dd steps
+// Every receiver of a class therefore sees the same arrival counts, and receivers of one class
+// evolve identically: a key's lifetime is two class states (honest fast receivers, honest slow
+// ones), and its deliveries at a step are whole honest classes, which the consensus pass reads as
+// two per-class key bitmaps per step.  So the keys created in a step are simulated one per lane
+// (lane L: a key of origin L), each as its two class states, the arrival counts in closed form
+// (simulate_batch; round 6: 4.6-5.4x on the many-round legs over one key per wave, which left the
+// scalar unit saturated).  A key's messages all land within 4 Dd steps
 // of its SEND (ECHO <= Dd, READY <= 3 Dd: a class READYs by quorum or is amplified by the other),
 // so RW = 32 covers Dd <= 8; the host uses this kernel only there (brc_engine.hip).
 //
@@ -370,8 +372,37 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // brc_step.h process_pair): opn = the cell is open and has arrivals, sa / ea / ra its SEND / ECHO / READY
     // arrivals, hS / hE / hR the key's message types landing now; es / rs / dl: ECHO / READY sent, delivered
     auto upd_cell = [&](uint32_t& fl, uint32_t& ec, uint32_t& rc, bool opn, uint32_t sa, uint32_t ea, uint32_t ra,
-                        bool hS, bool hE, bool hR, uint32_t& es, uint32_t& rs, uint32_t& dl) {
+                        bool hS, bool hE, bool hR, uint32_t& es, uint32_t& rs, uint32_t& dl, uint32_t& nr) {
         auto ge = [](uint32_t x, uint32_t y) -> uint32_t { return ((x - y) >> 31) ^ 1u; };   // x >= y (< 2^31)
+        if constexpr (CONN) {
+            // core/brbroadcast.py:60-119 with connection-identity peers (brc_step.h brb_cell_update_conn):
+            // sets count messages; the :119 amplification re-fires, nr READY copies this step.  In
+            // integer form (0/1 words, VALU): the bool form's per-lane conditions became SGPR lane
+            // masks combined with scalar ANDs, and this kernel is SALU-bound.
+            const uint32_t o = opn ? 1u : 0u, om = 0u - o;
+            es = o & sa & ~fl & 1u;                                   // :76-82 (F_EEX = bit 0)
+            fl |= es | (es << 3);
+            const uint32_t e = ea & om, eon = min(e, 1u);             // :84-98
+            const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
+            fl |= eon;
+            ec += e;
+            const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
+            fl |= r1 << 1;
+            const uint32_t x = ra & om, ron = min(x, 1u);             // :100-119
+            const uint32_t rexm = 0u - ((fl >> 1) & 1u);
+            const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
+            fl |= ron << 1;
+            rc += x;
+            const uint32_t any = ron & ge(rhi, rlo);
+            const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
+            const uint32_t fire = any & ~fl & ge(ahi, alo) & 1u;      // :118 (no F_RS test: re-fires)
+            nr = r1 + ((ahi - alo + 1u) & (0u - fire));
+            dl = any & ge(rhi, T_del);                                // :111-115
+            fl |= dl << 2;
+            rs = min(nr, 1u);
+            fl |= rs << 4;
+            return;
+        }
         if constexpr (BEB) {
             dl = (opn && sa) ? 1u : 0u;                             // brb_cell_update_beb
             fl |= dl << 2;
@@ -418,6 +449,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 rs |= r2;
             }
         }
+        nr = rs;
     };
     // ---- the lifetime of key slot k created at step t (wave-uniform): every step at which one of
     // its messages lands on an honest receiver, in order; cells in registers (brc_step.h C32 fields
@@ -518,38 +550,8 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                                     : nHF * (eA + rA) + nHS * (eB + rB) + (uint32_t)__popcll(sab);
             // a delivered cell ignores everything (core/brbroadcast.py:74)
             const bool opn = lane_in(hb) && !(fl & F_DEL);
-            auto ge = [](uint32_t x, uint32_t y) -> uint32_t { return ((x - y) >> 31) ^ 1u; };   // x >= y (< 2^31)
             uint32_t es = 0, rs = 0, dl = 0, nr = 0;
-            if constexpr (CONN) {
-                // core/brbroadcast.py:60-119 with connection-identity peers (brc_step.h brb_cell_update_conn):
-                // sets count messages; the :119 amplification re-fires, nr READY copies this step.  In
-                // integer form (0/1 words, VALU): the bool form's per-lane conditions became SGPR lane
-                // masks combined with scalar ANDs, and this kernel is SALU-bound.
-                const uint32_t o = opn ? 1u : 0u, om = 0u - o;
-                es = o & sa & ~fl & 1u;                                   // :76-82 (F_EEX = bit 0)
-                fl |= es | (es << 3);
-                const uint32_t e = ea & om, eon = min(e, 1u);             // :84-98
-                const uint32_t chk = min(e + (fl & 1u) - eon, 1u);
-                fl |= eon;
-                ec += e;
-                const uint32_t r1 = eon & chk & ge(ec, T_echo) & (~fl >> 1) & 1u;
-                fl |= r1 << 1;
-                const uint32_t x = ra & om, ron = min(x, 1u);             // :100-119
-                const uint32_t rexm = 0u - ((fl >> 1) & 1u);
-                const uint32_t rlo = 2u + ((rc - 1u) & rexm), rhi = x + (rc & rexm);
-                fl |= ron << 1;
-                rc += x;
-                const uint32_t any = ron & ge(rhi, rlo);
-                const uint32_t alo = max(rlo, T_amp), ahi = min(rhi, T_del - 1u);
-                const uint32_t fire = any & ~fl & ge(ahi, alo) & 1u;      // :118 (no F_RS test: re-fires)
-                nr = r1 + ((ahi - alo + 1u) & (0u - fire));
-                dl = any & ge(rhi, T_del);                                // :111-115
-                fl |= dl << 2;
-                rs = min(nr, 1u);
-                fl |= rs << 4;
-            } else {
-                upd_cell(fl, ec, rc, opn, sa, ea, ra, hS, hE, hR, es, rs, dl);
-            }
+            upd_cell(fl, ec, rc, opn, sa, ea, ra, hS, hE, hR, es, rs, dl, nr);
             const uint64_t eb = __ballot(es != 0), rbm = __ballot(rs != 0), db = __ballot(dl != 0);
             if (es) rE = r;
             if (!CONN && rs) rR = r;
@@ -638,7 +640,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
     // closed form), and the step statistics are wave sums over the batch.  The keys are independent, so
     // this is simulate(k) for every key of the batch at once: the same slot stamps, class delivery steps,
     // ring statistics and overflows, in VALU instead of the scalar unit, which simulate() saturates.
-    constexpr bool LANES = BRC_LIFE_LANES && !PL && !CONN;
+    constexpr bool LANES = BRC_LIFE_LANES && !PL;
     auto simulate_batch = [&](const bool has, const uint32_t k) {
         const bool vA = HF != 0, vB = HS != 0;
         const bool oF = laneF;                        // the origin is this lane
@@ -656,6 +658,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         uint32_t sent = 0xFFFFFFFFu;
         uint32_t last = t, dab = 0;
         const uint32_t kw = k >> 6;
+        // CONN: READY copies landing at steps r + j (j < 9): class A's in the low half, class B's in the high
+        uint32_t win[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) win[j] = 0;
 #pragma unroll 1
         for (uint32_t r = 1; ; ++r) {
             if (!__ballot(pend != 0u)) break;
@@ -675,19 +681,24 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 eB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
             }
             if (hR) {
-                const uint32_t xA = (sent >> 8) & 0xFFu, xB = sent >> 24;
-                rA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
-                rB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                if constexpr (CONN) {
+                    rA = win[0] & 0xFFFFu; rB = win[0] >> 16;
+                } else {
+                    const uint32_t xA = (sent >> 8) & 0xFFu, xB = sent >> 24;
+                    rA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                    rB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                }
             }
             const uint32_t saA = (hS && r == sdlA) ? 1u : 0u, saB = (hS && r == Dd) ? 1u : 0u;
             const uint32_t aA = act ? eA + rA + saA : 0u, aB = act ? eB + rB + saB : 0u;
             // a delivered cell ignores everything (core/brbroadcast.py:74)
             const bool opnA = vA && aA != 0 && !(flA & F_DEL), opnB = vB && aB != 0 && !(flB & F_DEL);
-            uint32_t esA = 0, rsA = 0, dlA = 0, esB = 0, rsB = 0, dlB = 0;
+            uint32_t esA = 0, rsA = 0, dlA = 0, esB = 0, rsB = 0, dlB = 0, nrA = 0, nrB = 0;
             if (act) {
-                upd_cell(flA, ecA, rcA, opnA, saA, eA, rA, hS, hE, hR, esA, rsA, dlA);
-                upd_cell(flB, ecB, rcB, opnB, saB, eB, rB, hS, hE, hR, esB, rsB, dlB);
+                upd_cell(flA, ecA, rcA, opnA, saA, eA, rA, hS, hE, hR, esA, rsA, dlA, nrA);
+                upd_cell(flB, ecB, rcB, opnB, saB, eB, rB, hS, hE, hR, esB, rsB, dlB, nrB);
             }
+            if (CONN) rsA = rsB = 0;                  // CONN: READY copies go through win, not send steps
             if (esA | rsA | esB | rsB) {
                 const uint32_t sm = (esA ? 0xFFu : 0u) | (rsA ? 0xFF00u : 0u) | (esB ? 0xFF0000u : 0u) | (rsB ? 0xFF000000u : 0u);
                 sent = (sent & ~sm) | ((r * 0x01010101u) & sm);
@@ -696,13 +707,23 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             // rsB)), cells nHF [aA > 0] + nHS [aB > 0], deliveries nHF dlA + nHS dlB (simulate()'s popcounts)
             const uint64_t am = __ballot(act);
             if (am) {
-                const uint32_t s1 = wave_sum(aA | (aB << 16));
-                const uint32_t s2 = wave_sum((esA + rsA) | ((esB + rsB) << 8) | ((aA != 0 ? 1u : 0u) << 16) |
-                                             ((aB != 0 ? 1u : 0u) << 24));
+                uint32_t arr, msgs, cells;
+                if constexpr (CONN) {
+                    // READY copies: a count may reach 64 x 64 per lane, so the sums take whole words
+                    const uint32_t sA = wave_sum(aA), sB = wave_sum(aB);
+                    const uint32_t s2 = wave_sum((esA + nrA) | ((esB + nrB) << 16));
+                    arr = nHF * sA + nHS * sB;
+                    msgs = n * (nHF * (s2 & 0xFFFFu) + nHS * (s2 >> 16));
+                    cells = nHF * (uint32_t)__popcll(__ballot(aA != 0)) + nHS * (uint32_t)__popcll(__ballot(aB != 0));
+                } else {
+                    const uint32_t s1 = wave_sum(aA | (aB << 16));
+                    const uint32_t s2 = wave_sum((esA + rsA) | ((esB + rsB) << 8) | ((aA != 0 ? 1u : 0u) << 16) |
+                                                 ((aB != 0 ? 1u : 0u) << 24));
+                    arr = nHF * (s1 & 0xFFFFu) + nHS * (s1 >> 16);
+                    msgs = n * (nHF * (s2 & 0xFFu) + nHS * ((s2 >> 8) & 0xFFu));
+                    cells = nHF * ((s2 >> 16) & 0xFFu) + nHS * (s2 >> 24);
+                }
                 const uint32_t ndA = (uint32_t)__popcll(__ballot(dlA != 0)), ndB = (uint32_t)__popcll(__ballot(dlB != 0));
-                const uint32_t arr = nHF * (s1 & 0xFFFFu) + nHS * (s1 >> 16);
-                const uint32_t msgs = n * (nHF * (s2 & 0xFFu) + nHS * ((s2 >> 8) & 0xFFu));
-                const uint32_t cells = nHF * ((s2 >> 16) & 0xFFu) + nHS * (s2 >> 24);
                 const uint32_t dels = nHF * ndA + nHS * ndB;
                 const bool mine = lane == row;
                 rg_arr += mine ? arr : 0u; rg_msg += mine ? msgs : 0u;
@@ -731,6 +752,21 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             if (rsA || rsB) {
                 if (rsA) pend |= 1u << 21;
                 if (vB || rsB) pend |= 1u << (20u + Dd);
+            }
+            if constexpr (CONN) {
+                // copies sent now: class A's land on A after 1 step, every other pair's after Dd
+                if (nrA || nrB) {
+                    const uint32_t cF = nHF * nrA, cS = nHS * nrB;
+                    win[1] += cF;
+                    const uint32_t cd = cS + ((cF + cS) << 16);
+#pragma unroll
+                    for (int j = 1; j < 9; ++j) win[j] += (uint32_t)j == Dd ? cd : 0u;
+                    if (nrA) pend |= 1u << 21;
+                    if (vB) pend |= 1u << (20u + Dd);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) win[j] = win[j + 1];
+                win[8] = 0;
             }
             if (act) last = ts;
             pend = (pend >> 1) & ~((1u << 9) | (1u << 19));   // step r consumed: the window moves to r + 1

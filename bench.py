@@ -14,7 +14,7 @@ scaling); the only collective is one RCCL all-reduce of the statistics.
 
 Legs, one JSON line (rank 0); each leg is one launch per step at 2^20 instances:
   reference  the protocol exactly as the reference runs it (quirks included) -- the headline
-             `value`.  Its coin branch is dead, so split proposals decide "-1" in
+             `value`, on the step kernel (per-receiver cells: the general path).  Its coin branch is dead, so split proposals decide "-1" in
              round 1; `decided_value_hist` shows that share.
   spec       the protocol the reference intends, with the common coin made reachable (SURVEY §8
              F3): "many coin rounds".  Its phase window Q = 8 doubles the key slots; with 4-B cells
@@ -30,6 +30,12 @@ Legs, one JSON line (rank 0); each leg is one launch per step at 2^20 instances:
   long       the reference protocol to SURVEY cfg4's round cap 64 (key window 128: ~7,600 keys of one
              instance live at once by round 64), key-lifetime kernel, 2^20 instances in one launch.
   spec64     SPEC to round cap 64: 64 decisions per replica, coin rounds included, step kernel.
+  ref2c      the reference leg's workload on the key-lifetime kernel's two-class form: under slow-set
+             delays a key's honest receivers of one class evolve identically, so the kernel simulates a
+             key's whole lifetime as two class states, one key per lane (csrc/brc_life.h).  Exact for
+             this delay model only (the engine's default kernel for it, same results as the step kernel:
+             tests/test_gpu_fullsize.py); the headline stays on the general step kernel.
+  spec2c     the spec leg's workload on the same two-class form.
 The legs of seconds per step (many, long, spec64) time at most LEG_STEPS of --steps / --warmup
 and report the counts they timed.
 """
@@ -50,14 +56,18 @@ HBM_PEAK_GBS = 8000.0                                           # MI355X_MICROAR
 SPEC_TILE = 1 << 20                                             # SPEC (Q = 8) instances per engine tile
 MANY_CAP = 8                                                    # the many leg's round cap
 LONG_CAP = 64                                                   # SURVEY cfg4's round cap (long, spec64 legs)
-# leg -> (protocol mode, peer mode, delay model, delay max, key window)
-LEGS = {"reference": ("reference", "sender", "slowset", DELAY_MAX, 4),
-        "spec": ("spec", "sender", "slowset", DELAY_MAX, 8),
-        "conn": ("reference", "connection", "slowset", DELAY_MAX, 4),
-        "connu": ("reference", "connection", "uniform", 2, 4),
-        "many": ("reference", "sender", "slowset", DELAY_MAX, 32),
-        "long": ("reference", "sender", "slowset", DELAY_MAX, 128),
-        "spec64": ("spec", "sender", "slowset", DELAY_MAX, 8)}
+# leg -> (protocol mode, peer mode, delay model, delay max, key window, kernel).  kernel: "step" pins the
+# step kernel (per-receiver cells, any delay model: the general path the headline measures), "life" the
+# key-lifetime kernel, None the engine's own choice (include/brc.h brc_last_kernel)
+LEGS = {"reference": ("reference", "sender", "slowset", DELAY_MAX, 4, "step"),
+        "spec": ("spec", "sender", "slowset", DELAY_MAX, 8, "step"),
+        "conn": ("reference", "connection", "slowset", DELAY_MAX, 4, None),
+        "connu": ("reference", "connection", "uniform", 2, 4, None),
+        "many": ("reference", "sender", "slowset", DELAY_MAX, 32, None),
+        "long": ("reference", "sender", "slowset", DELAY_MAX, 128, None),
+        "spec64": ("spec", "sender", "slowset", DELAY_MAX, 8, "step"),
+        "ref2c": ("reference", "sender", "slowset", DELAY_MAX, 4, "life"),
+        "spec2c": ("spec", "sender", "slowset", DELAY_MAX, 8, "life")}
 # legs with a round cap of their own (the others take --round-cap)
 LEG_CAP = {"many": MANY_CAP, "long": LONG_CAP, "spec64": LONG_CAP}
 # legs of seconds per step time at most this many (steps, warmup) of --steps / --warmup, so that the default
@@ -71,11 +81,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--instances", type=int, default=1 << 20, help="instances per GPU (SURVEY §8(d) cfg4: 2^20)")
-    ap.add_argument("--legs", default="reference,spec,conn,connu,many,long,spec64",
+    ap.add_argument("--legs", default="reference,spec,conn,connu,many,long,spec64,ref2c,spec2c",
                     help="comma list of reference (the headline value), spec (SURVEY §8 F3 coin rounds), conn "
                          "(connection-identity peers, what the shipped reference runs: SURVEY §8 F1), connu (the same "
                          "under per-link uniform[1,2] delays), many (the reference protocol to round cap 8), long (the "
-                         "reference protocol to SURVEY cfg4's round cap 64) and spec64 (SPEC to round cap 64)")
+                         "reference protocol to SURVEY cfg4's round cap 64), spec64 (SPEC to round cap 64), ref2c / "
+                         "spec2c (reference / spec on the key-lifetime kernel's two-class form)")
     ap.add_argument("--mode", choices=tuple(LEGS), default=None,
                     help="shorthand for --legs <mode> (the headline leg is the first one run)")
     ap.add_argument("--round-cap", type=int, default=1, help="round cap of every leg but many")
@@ -97,7 +108,7 @@ def cpu_baseline(seconds, leg="reference", round_cap=1):
     """The C oracle (a scalar port of the reference's path) on the same workload, one thread per
     core (ctypes releases the GIL inside the C run): threads take interleaved global instance ids
     from 0 and run until `seconds` have passed.  Counters only (the oracle's light mode)."""
-    mode, peer, model, dmax, window = LEGS[leg]
+    mode, peer, model, dmax, window, _kernel = LEGS[leg]
     import concurrent.futures
     from oracle import oracle
     from tests.golden import specs as S
@@ -159,13 +170,21 @@ def load_profile(instances, kernel_ms, mode="reference", cell_bytes=CELL_BYTES):
 def make_engine(leg, count, first, device, round_cap):
     from byzantinerandomizedconsensus_amd import _lib as L
     from byzantinerandomizedconsensus_amd.engine import Engine
-    mode, peer, model, dmax, window = LEGS[leg]
+    mode, peer, model, dmax, window, kernel = LEGS[leg]
     spec = mode == "spec"
-    return Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
-                  delay_model={"slowset": L.DELAY_SLOWSET, "uniform": L.DELAY_UNIFORM}[model], delay_max=dmax,
-                  round_cap=round_cap, step_cap=4000, key_window=window, variants=1, proposals=L.PROPOSALS_PHILOX,
-                  instance_offset=first, device=device, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
-                  coin_seed=COIN_SEED, peer_mode=L.PEER_CONNECTION if peer == "connection" else L.PEER_SENDER)
+    old = os.environ.pop("BRC_KERNEL", None)       # read by brc_create only
+    if kernel:
+        os.environ["BRC_KERNEL"] = kernel
+    try:
+        return Engine(n=N_REPLICAS, f=F_FAULTS, instances=count, protocol="consensus", seed=SEED,
+                      delay_model={"slowset": L.DELAY_SLOWSET, "uniform": L.DELAY_UNIFORM}[model], delay_max=dmax,
+                      round_cap=round_cap, step_cap=4000, key_window=window, variants=1, proposals=L.PROPOSALS_PHILOX,
+                      instance_offset=first, device=device, mode=L.MODE_SPEC if spec else L.MODE_REFERENCE,
+                      coin_seed=COIN_SEED, peer_mode=L.PEER_CONNECTION if peer == "connection" else L.PEER_SENDER)
+    finally:
+        os.environ.pop("BRC_KERNEL", None)
+        if old is not None:
+            os.environ["BRC_KERNEL"] = old
 
 
 def collect(eng):
@@ -331,8 +350,13 @@ def parity_basis(leg):
 
 
 def workload_name(leg, cap, per):
-    proto, peer, model, dmax, window = LEGS[leg]
+    proto, peer, model, dmax, window, kernel = LEGS[leg]
     form = ""
+    if kernel == "step":
+        form = ", step kernel (per-receiver cells: the general path, any delay model)"
+    elif kernel == "life" and peer == "sender" and model == "slowset":
+        form = (", key-lifetime kernel, two-class form (slow-set symmetry: a key's lifetime as two receiver-class "
+                "states, exact for this delay model only)")
     if peer == "connection":
         # the key-lifetime kernel's two forms (csrc/brc_life.h): under slow-set delays the receivers of one
         # class see the same arrivals, so it counts them once per class -- exact for that model only

@@ -447,9 +447,11 @@ int brc_create(const brc_config* cfg, void** out) {
     e->cons_bytes = cons_bytes_per_item(spec, e->wide, e->lpi, e->msize, c.key_window, c.variants, e->nval);
     // key-lifetime kernel (brc_life.h): NPAD = 64 consensus under a two-class delay model with D <= 8
     // or per-link (uniform / geometric) delays with D <= 8, proposals from Philox or loaded, no event
-    // log, no Byzantine pattern.  BRC_KERNEL=step | life | auto (default): auto runs connection-identity
-    // peers on it (their step-kernel cells are 5 words); sender peers stay on the step kernel, which is
-    // faster there
+    // log, no Byzantine pattern.  BRC_KERNEL=step | life | auto (default): auto runs it whenever the
+    // configuration is eligible, except sender peers under per-link delays (the step kernel is faster
+    // there): since round 6 its two-class form simulates a step's new keys one per lane, 1.8-7x faster than
+    // the step kernel on cfg4.  A run it cannot take (injections, an event log, a stepped run)
+    // falls back to the step kernel.
     // The lifetime kernel keeps no cells, so it also runs sender peers whose step-kernel cell store
     // would not fit in the free device memory (the reference protocol's many-round runs: its phase
     // leakage keeps ~1,000 keys of one instance live by round 8 at n = 64) and the key
@@ -478,7 +480,8 @@ int brc_create(const brc_config* cfg, void** out) {
             if (hipMemGetInfo(&fr, &tot) == hipSuccess && need > tot / 10 * 9) big = true;
             (void)hipGetLastError();
         }
-        e->life_cfg = eligible && !force_step && (force_life || c.peer_mode == BRC_PEER_CONNECTION || big);
+        const bool prefer_life = c.peer_mode == BRC_PEER_CONNECTION || !e->life_pl;
+        e->life_cfg = eligible && !force_step && (force_life || prefer_life || big);
         e->step_ok = !big;
         if (big && !e->life_cfg) {
             g_create_err = c.key_window * c.variants > 32

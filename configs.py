@@ -19,6 +19,8 @@ Workloads:
   cfg4-ref-r8  the reference protocol to round cap 8 (bench.py's many leg: the key-lifetime kernel), 2^20
   cfg4-ref-r64, cfg4-spec-r64  SURVEY cfg4's round cap 64 (bench.py's long / spec64 legs), 2^20
   cfg4-conn-geometric  connection peers under geometric delays capped at 16 (64-row ring), 2^20
+  cfg4-{ref,spec,beb,spec-r64}-2c  the sender-peer cfg4 rows above (which pin the step kernel) on the
+             key-lifetime kernel's two-class form, the engine's default for them (slow-set symmetry)
   cfg5-*     n=256 f=85 SPEC, 6144 instances per GPU, const / uniform[1,4] / geometric<=16
   cfg5-conn-uniform  n=256 f=85, connection-identity peers (the reference as shipped), reference
              protocol, uniform[1,4] delays, 6144 instances per GPU (the wide kernel's 40-B cells)
@@ -59,10 +61,13 @@ def workloads(L):
         "cfg3-spec": (1000000, False, dict(base, n=16, f=5, seed=0x5EED0003, delay_model=uni, delay_max=4,
                                            round_cap=1, key_window=4, variants=2, byz_pattern=L.BYZ_EQUIVOCATE,
                                            byzantine=list(range(11, 16)), mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
+        # kernel="step": the step kernel (per-receiver cells, the general path the bench headline measures);
+        # the engine's default for these two-class configurations is the key-lifetime kernel (the -2c rows)
         "cfg4-ref": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
-                                         round_cap=1, key_window=4)),
+                                         round_cap=1, key_window=4, kernel="step")),
         "cfg4-spec": (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
-                                          round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED)),
+                                          round_cap=1, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED,
+                                          kernel="step")),
     }
     # cfg4 under the peer identity the shipped reference runs (core/brbroadcast.py:69: every message
     # is a new connection, no duplicate suppression; 5-word cells) and over best-effort broadcast
@@ -75,7 +80,7 @@ def workloads(L):
             1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=1, delay_max=dmax, round_cap=1,
                                 key_window=4, peer_mode=L.PEER_CONNECTION))
     W["cfg4-beb"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
-                                         round_cap=1, key_window=8, mode=L.MODE_BEB))
+                                         round_cap=1, key_window=8, mode=L.MODE_BEB, kernel="step"))
     # the reference protocol to round cap 8 (bench.py's many leg; the key-lifetime kernel at 2^20)
     W["cfg4-ref-r8"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                             round_cap=8, key_window=32))
@@ -84,7 +89,13 @@ def workloads(L):
     W["cfg4-ref-r64"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
                                              round_cap=64, key_window=128))
     W["cfg4-spec-r64"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=slow, delay_max=8,
-                                              round_cap=64, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED))
+                                              round_cap=64, key_window=8, mode=L.MODE_SPEC, coin_seed=COIN_SEED,
+                                              kernel="step"))
+    # the same sender-peer cfg4 workloads on the key-lifetime kernel's two-class form (the engine's default
+    # for them since round 6): a key's lifetime as two receiver-class states, exact under slow-set delays
+    for nm in ("cfg4-ref", "cfg4-spec", "cfg4-beb", "cfg4-spec-r64"):
+        sz, per, kw = W[nm]
+        W[nm + "-2c"] = (sz, per, dict(kw, kernel="life"))
     # connection peers under cfg5's geometric delays capped at 16 (the per-link form's 64-row ring)
     W["cfg4-conn-geometric"] = (1 << 20, True, dict(base, n=64, f=21, seed=0x5EED0004, delay_model=3, delay_max=16,
                                                     round_cap=1, key_window=4, peer_mode=L.PEER_CONNECTION))
@@ -110,7 +121,8 @@ def cell_bytes(n, peer_mode=0):
 
 # configs.py workloads that are bench.py legs: their profiles are the bench's (workload "cfg4", mode = leg)
 BENCH_LEGS = {"cfg4-ref": "reference", "cfg4-spec": "spec", "cfg4-conn": "conn", "cfg4-conn-uniform-d2": "connu",
-              "cfg4-ref-r8": "many", "cfg4-ref-r64": "long", "cfg4-spec-r64": "spec64"}
+              "cfg4-ref-r8": "many", "cfg4-ref-r64": "long", "cfg4-spec-r64": "spec64", "cfg4-ref-2c": "ref2c",
+              "cfg4-spec-2c": "spec2c"}
 
 
 def measured_profile(name, kernel_ms):
@@ -233,7 +245,18 @@ def main():
         first, count = shard.shard_range(size * world if per_gpu else size, world, rank)
         n = kw["n"]
         bpc = 6 * ((n + 7) // 8) + 2
-        with Engine(instances=count, instance_offset=first, device=local, **kw) as eng:
+        kw = dict(kw)
+        kernel = kw.pop("kernel", None)             # pin a kernel (BRC_KERNEL, read by brc_create)
+        old = os.environ.pop("BRC_KERNEL", None)
+        if kernel:
+            os.environ["BRC_KERNEL"] = kernel
+        try:
+            eng = Engine(instances=count, instance_offset=first, device=local, **kw)
+        finally:
+            os.environ.pop("BRC_KERNEL", None)
+            if old is not None:
+                os.environ["BRC_KERNEL"] = old
+        with eng:
             for _ in range(args.warmup):
                 eng.reset()
                 eng.run()

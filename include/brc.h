@@ -210,11 +210,12 @@ int brc_last_kernel_ms(void* engine, float* ms);
  * delay_max <= 8 (its two-class form) or uniform / geometric delays with delay_max <= 16 (its
  * per-link form, which keeps a delivery-bitmap ring in HBM: 64 KB per instance at NK = 256, 128 KB
  * for delays above 8), no event log, no byz_pattern, no injections, max_steps == 0.  By default it
- * runs connection-identity peers (BRC_PEER_CONNECTION), and sender peers whose step-kernel state
- * (cells, slot arrays, activity ring) would exceed 90 % of the device's TOTAL memory -- a choice fixed
- * by the configuration and device model, not by what else holds memory -- or whose key window is
- * above 32; such an engine is lifetime-kernel-only: brc_inject returns BRC_E_UNSUPPORTED and so does a
- * run with max_steps > 0.  Before the first brc_run, brc_last_kernel reports the kernel a fresh run to
+ * runs every such configuration except sender peers under uniform / geometric delays (the step kernel
+ * is faster there); a run it cannot take (injections, max_steps > 0) goes to the step kernel.  Sender
+ * peers whose step-kernel state (cells, slot arrays, activity ring) would exceed 90 % of the device's
+ * TOTAL memory -- a choice fixed by the configuration and device model, not by what else holds memory
+ * -- or whose key window is above 32 are lifetime-kernel-only: brc_inject returns BRC_E_UNSUPPORTED
+ * and so does a run with max_steps > 0.  Before the first brc_run, brc_last_kernel reports the kernel a fresh run to
  * completion would launch.  The environment variable
  * BRC_KERNEL (read by brc_create) = life uses it for every eligible engine, = step never.  Its
  * results equal the step kernel's; its instances end final, so a later injection that would

@@ -259,7 +259,7 @@ def test_cfg4_long_consensus_many_rounds(mode):
     ids = sorted(random.Random(8).sample(range(N), 5)) + [N - 1]
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
-        assert eng.last_kernel() == ("step" if spec else "life")
+        assert eng.last_kernel() == "life"              # two-class form (SPEC too, round 6)
         st = eng.stats()
         hist = eng.round_histogram(66)
         res = {i: eng.instances_result(i, 1)[0] for i in ids}
@@ -312,7 +312,7 @@ def test_cfg4_round_cap_64_2p20_bench_legs(leg):
     instances per GPU, one launch each.  long: the reference protocol (the re-proposal loop
     core/byzantinerandomizedconsensus.py:96-106; by round 64 ~7,600 keys of one instance are live at
     once, so the key-lifetime kernel with a key window of 128, its slot metadata in HBM).  spec64: the
-    intended protocol with the common coin (:88-92 made reachable) on the step kernel, window 8.
+    intended protocol with the common coin (:88-92 made reachable), window 8, on the same kernel.
     Sampled ids equal the oracle (counters incl. cell-steps, every replica's first and last decision
     and its decide count)."""
     L = _L()
@@ -324,7 +324,7 @@ def test_cfg4_round_cap_64_2p20_bench_legs(leg):
     ids = sorted(random.Random(6464 + spec).sample(range(N - 1), 5)) + [N - 1]
     with _engine(instance_offset=0, instances=N, **kw) as eng:
         eng.run()
-        assert eng.last_kernel() == ("step" if spec else "life")
+        assert eng.last_kernel() == "life"              # two-class form (SPEC too, round 6)
         st = eng.stats()
         vals, dis = eng.decisions()
         res = {i: eng.instances_result(i, 1)[0] for i in ids}
@@ -403,8 +403,8 @@ def _batch_digest(eng, chunk=1 << 16):
 
 
 def test_cfg4_2p20_step_kernel_equals_lifetime_kernel():
-    """The bench's whole 2^20 sender-peer cfg4 batch on both kernels (BRC_KERNEL=step: the
-    headline's cell store; BRC_KERNEL=life: the key-lifetime kernel, cells in registers): a digest
+    """The bench's whole 2^20 sender-peer cfg4 batch on both kernels (BRC_KERNEL=step: the step
+    kernel's cell store; BRC_KERNEL=life: the key-lifetime kernel the headline runs, cells in registers): a digest
     of every instance's counters (cell-steps included: the roofline's unit) and every replica's
     consensus record is identical -- not a sample, the whole batch (reference:
     core/brbroadcast.py:60-119, core/byzantinerandomizedconsensus.py:53-106)."""

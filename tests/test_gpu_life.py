@@ -3,7 +3,7 @@
 The engine runs a fresh, eligible configuration (n in 33..64, consensus, constant or slow-set
 delays (two-class form) or uniform / geometric delays (per-link form) with D <= 8, no events, no
 injections; include/brc.h brc_last_kernel) on the lifetime
-kernel: by default with connection-identity peers, with sender peers when BRC_KERNEL=life.  The
+kernel: by default, except sender peers under per-link delays (there only when BRC_KERNEL=life).  The
 step kernel is pinned to the reference fixtures (test_gpu_parity.py), so each workload here runs on
 both kernels (BRC_KERNEL=life / step at engine creation) and every output must match: per-instance status, last active
 step, message / arrival / cell-step / delivery counters, every replica's consensus record, the
@@ -210,13 +210,18 @@ def test_lifetime_only_engine_rejects_injections_up_front():
         assert eng.last_kernel() == "life"
         assert all(r["status"] == "done" for r in eng.instances_result())
     with Engine(instances=4, **dict(kw, key_window=8)) as eng:
+        # a window the step kernel takes: the lifetime kernel by default, and an injection moves the run
+        # to the step kernel instead of being refused
+        assert eng.last_kernel() == "life"
+        eng.inject([dict(t=0, kind=L.INJ_PROPOSE, instance=0, node=0, value=1)])
+        eng.run()
         assert eng.last_kernel() == "step"
 
 
 def test_kernel_choice():
-    """Default choice: connection peers run on the lifetime kernel, sender peers on the step kernel
-    (faster there); event logs, injections, stepped runs and two-class delays past 8 stay on the step kernel;
-    a lifetime-run instance cannot be re-opened by an injection."""
+    """Default choice: eligible configurations run on the lifetime kernel, except sender peers under
+    per-link delays (step kernel, faster there); event logs, injections, stepped runs and two-class delays
+    past 8 stay on the step kernel; a lifetime-run instance cannot be re-opened by an injection."""
     from byzantinerandomizedconsensus_amd.engine import Engine
     L = _L()
     assert "BRC_KERNEL" not in os.environ
@@ -227,7 +232,10 @@ def test_kernel_choice():
         st = eng.instances_result()
     with Engine(instances=4, **_workloads()["ref-slow64"]) as eng:
         eng.run()
-        assert eng.last_kernel() == "step"
+        assert eng.last_kernel() == "life"                # sender peers, two-class form
+    with Engine(instances=4, **_workloads()["ref-unif64-d2-r3"]) as eng:
+        eng.run()
+        assert eng.last_kernel() == "step"                # sender peers, per-link delays
     with Engine(instances=4, event_capacity=1 << 16, **kw) as eng:
         eng.run()
         assert eng.last_kernel() == "step"

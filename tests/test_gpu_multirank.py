@@ -47,7 +47,7 @@ def _run(cmd, timeout):
 
 def _legs(d):
     out = {"reference": {k: d[k] for k in KEYS}}
-    for leg in ("spec", "many", "long", "spec64"):
+    for leg in ("spec", "many", "long", "spec64", "ref2c", "spec2c"):
         if leg + "_leg" in d:
             out[leg] = {k: d[leg + "_leg"][k] for k in KEYS}
     return out
@@ -55,7 +55,7 @@ def _legs(d):
 
 @pytest.mark.gpu
 def test_two_ranks_equal_one_rank_over_the_same_global_ids():
-    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many,long,spec64"]
+    bench_args = ["--steps", "1", "--warmup", "0", "--no-cpu", "--legs", "reference,spec,many,long,spec64,ref2c,spec2c"]
     multi = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(WORLD),
                   "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
                   "--gpus", str(WORLD), "--backend", "gloo", "--instances", str(PER_RANK)] + bench_args, 300)
@@ -63,10 +63,17 @@ def test_two_ranks_equal_one_rank_over_the_same_global_ids():
     assert multi["n_gpus"] == WORLD and single["n_gpus"] == 1
     assert multi["config"]["instances_per_gpu"] * WORLD == single["config"]["instances_per_gpu"]
     m, s = _legs(multi), _legs(single)
-    for leg in ("reference", "spec", "many", "long", "spec64"):
+    for leg in ("reference", "spec", "many", "long", "spec64", "ref2c", "spec2c"):
         assert m[leg]["counts"]["instances"] == PER_RANK * WORLD
         assert m[leg]["counts"]["decided"] > 0
         assert m[leg] == s[leg], leg
+    # the two-class lifetime legs run the step-kernel legs' workloads: the same results (lane_loads and max_t
+    # are kernel-specific: the step kernel's row loads and last touched step)
+    for a, b in (("reference", "ref2c"), ("spec", "spec2c")):
+        ca = {k: v for k, v in s[a]["counts"].items() if k not in ("lane_loads", "max_t")}
+        cb = {k: v for k, v in s[b]["counts"].items() if k not in ("lane_loads", "max_t")}
+        assert ca == cb and {k: v for k, v in s[a].items() if k != "counts"} == \
+            {k: v for k, v in s[b].items() if k != "counts"}, (a, b)
 
 
 @pytest.mark.gpu

@@ -23,6 +23,7 @@ if which in ("reference", "spec"):
 else:
     import configs
     _size, _per, kw = configs.workloads(L)[which]
+    kw = {k: v for k, v in kw.items() if k != "kernel"}
     eng = Engine(instances=inst, **kw)
 lib = ctypes.CDLL(os.environ["BRC_LIB"])
 out = (ctypes.c_ulonglong * 12)()

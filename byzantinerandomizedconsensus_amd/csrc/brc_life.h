@@ -61,6 +61,9 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 #ifndef BRC_LIFE_LANES
 #define BRC_LIFE_LANES 1   // two-class form, sender peers: the new keys' lifetimes simulated one key per lane
 #endif
+#ifndef BRC_LIFE_BSTAT
+#define BRC_LIFE_BSTAT 0   // LANES, sender peers: the batch's step statistics by ballot popcounts instead of wave sums
+#endif
 #ifndef BRC_LIFE_LANES_WAVES
 #define BRC_LIFE_LANES_WAVES 8   // their waves per SIMD
 #endif
@@ -675,18 +678,23 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             const uint32_t c1 = r - 1u, cD = r >= Dd ? r - Dd : 0x100u;   // 0x100: matches no byte
             // class arrivals: fast senders (class A) land on A after 1 step, every other pair after Dd
             uint32_t eA = 0, eB = 0, rA = 0, rB = 0;
+            // which class sent now-landing messages: e1 / q1 A's ECHO / READY sent at r - 1, e3 / q3 at
+            // r - Dd, e2 / q2 B's at r - Dd
+            bool e1 = false, e2 = false, e3 = false, q1 = false, q2 = false, q3 = false;
             if (hE) {
                 const uint32_t xA = sent & 0xFFu, xB = (sent >> 16) & 0xFFu;
-                eA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
-                eB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                e1 = xA == c1; e2 = xB == cD; e3 = xA == cD;
+                eA = (e1 ? nHF : 0u) + (e2 ? nHS : 0u);
+                eB = (e3 ? nHF : 0u) + (e2 ? nHS : 0u);
             }
             if (hR) {
                 if constexpr (CONN) {
                     rA = win[0] & 0xFFFFu; rB = win[0] >> 16;
                 } else {
                     const uint32_t xA = (sent >> 8) & 0xFFu, xB = sent >> 24;
-                    rA = (xA == c1 ? nHF : 0u) + (xB == cD ? nHS : 0u);
-                    rB = (xA == cD ? nHF : 0u) + (xB == cD ? nHS : 0u);
+                    q1 = xA == c1; q2 = xB == cD; q3 = xA == cD;
+                    rA = (q1 ? nHF : 0u) + (q2 ? nHS : 0u);
+                    rB = (q3 ? nHF : 0u) + (q2 ? nHS : 0u);
                 }
             }
             const uint32_t saA = (hS && r == sdlA) ? 1u : 0u, saB = (hS && r == Dd) ? 1u : 0u;
@@ -715,6 +723,15 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     arr = nHF * sA + nHS * sB;
                     msgs = n * (nHF * (s2 & 0xFFFFu) + nHS * (s2 >> 16));
                     cells = nHF * (uint32_t)__popcll(__ballot(aA != 0)) + nHS * (uint32_t)__popcll(__ballot(aB != 0));
+                } else if constexpr (BRC_LIFE_BSTAT) {
+                    // the sums as popcounts of ballots: a lane's class counts are class sizes times conditions
+                    auto pc = [&](bool c) -> uint32_t { return (uint32_t)__popcll(__ballot(act && c)); };
+                    const uint32_t n2 = pc(e2) + pc(q2);
+                    const uint32_t sA = nHF * (pc(e1) + pc(q1)) + nHS * n2 + pc(saA != 0);
+                    const uint32_t sB = nHF * (pc(e3) + pc(q3)) + nHS * n2 + pc(saB != 0);
+                    arr = nHF * sA + nHS * sB;
+                    msgs = n * (nHF * (pc(esA != 0) + pc(rsA != 0)) + nHS * (pc(esB != 0) + pc(rsB != 0)));
+                    cells = nHF * pc(aA != 0) + nHS * pc(aB != 0);
                 } else {
                     const uint32_t s1 = wave_sum(aA | (aB << 16));
                     const uint32_t s2 = wave_sum((esA + rsA) | ((esB + rsB) << 8) | ((aA != 0 ? 1u : 0u) << 16) |
@@ -926,18 +943,39 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
             }
             return bits;
         };
+        // HM: the next key word >= w the step's summary flags (NOKEY: none) -- the consensus passes visit only
+        // those, and read each one's slot metadata one flagged word (group) AHEAD, so the HBM round trip of
+        // the next word overlaps the deliveries of this one (no SEND changes the metadata during the pass)
+        auto next_flagged = [&](uint32_t w) -> uint32_t {
+            if (w < 64) { const uint64_t x = fw[0] & (~0ull << w); if (x) return (uint32_t)__builtin_ctzll(x); w = 64; }
+            if (w < 128) { const uint64_t x = fw[1] & (~0ull << (w - 64)); if (x) return 64u + (uint32_t)__builtin_ctzll(x); }
+            return NOKEY;
+        };
         if constexpr (QBIG) {
             // key windows of 64 / 128 (the reference protocol's many-round runs): a key prefix
             // (origin, variant) spans Q / 64 whole words; its deliveries of one step (one origin) go one
             // at a time, smallest phase index first -- the canonical (kp, s) order
             const uint32_t wpg = Q > 64 ? Q / 64 : 1u;
+            uint32_t gw = next_flagged(0);
+            if (gw != NOKEY) gw &= ~(wpg - 1u);                       // the flagged word's group
+            uint32_t pf0 = 0, pf1 = 0;                                // the group's metadata words, in flight
+            if (gw != NOKEY) {
+                pf0 = mld(gw * 64 + lane);
+                if (wpg > 1) pf1 = mld((gw + 1) * 64 + lane);
+            }
 #pragma unroll 1
-            for (uint32_t w = 0; w < nkw; w += wpg) {
+            while (gw != NOKEY) {
+                const uint32_t w = gw, m0 = pf0, m1 = pf1;
+                gw = next_flagged(w + wpg);
+                if (gw != NOKEY) {
+                    gw &= ~(wpg - 1u);
+                    pf0 = mld(gw * 64 + lane);
+                    if (wpg > 1) pf1 = mld((gw + 1) * 64 + lane);
+                }
                 uint64_t gb[2] = {dword(w), wpg > 1 ? dword(w + 1) : 0ull};
                 if (!__ballot((gb[0] | gb[1]) != 0)) continue;
-                // the group's slot metadata, one coalesced read per word (no SEND changes it during the pass)
-                s_sv[lane] = mld(w * 64 + lane) & 0xFFFFu;
-                if (wpg > 1) s_sv[64 + lane] = mld((w + 1) * 64 + lane) & 0xFFFFu;
+                s_sv[lane] = m0 & 0xFFFFu;
+                if (wpg > 1) s_sv[64 + lane] = m1 & 0xFFFFu;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                 while (gb[0] | gb[1]) {
                     uint32_t bs = 0xFFFFFFFFu, bk = 0;
@@ -953,13 +991,23 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 }
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             }
-        } else
+        } else {
+        uint32_t pfw = NOKEY, pf = 0;                 // HM: the next flagged word and its metadata, in flight
+        if (HM) {
+            pfw = next_flagged(0);
+            if (pfw != NOKEY) pf = mld(pfw * 64 + lane);
+        }
 #pragma unroll 1
-        for (uint32_t w = 0; w < nkw; ++w) {
+        for (uint32_t w = HM ? pfw : 0u; w < nkw; w = HM ? pfw : w + 1u) {
             uint64_t bits = dword(w);
-            if (HM && __ballot(bits != 0)) {           // the word's slot metadata, one coalesced read
-                s_sv[lane] = mld(w * 64 + lane) & 0xFFFFu;
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (HM) {
+                const uint32_t m = pf;
+                pfw = next_flagged(w + 1u);
+                if (pfw != NOKEY) pf = mld(pfw * 64 + lane);
+                if (__ballot(bits != 0)) {             // the word's slot metadata (read one flagged word ahead)
+                    s_sv[lane] = m & 0xFFFFu;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                }
             }
             if constexpr (SPEC) {
                 // word at once when every delivering lane is at one phase index c0 and its current-phase
@@ -1039,6 +1087,7 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 else cons_deliver_vh(snap_w(w * 64 + best) >> 14, (w * 64 + best) >> ksh);
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        }
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         LIFE_STAMP(2);

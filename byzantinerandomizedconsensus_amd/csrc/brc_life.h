@@ -61,6 +61,9 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 #ifndef BRC_LIFE_LANES
 #define BRC_LIFE_LANES 1   // two-class form, sender peers: the new keys' lifetimes simulated one key per lane
 #endif
+#ifndef BRC_LIFE_QBULK
+#define BRC_LIFE_QBULK 1   // key windows of 64 / 128: a lane's deliveries of one origin at once when no phase can end
+#endif
 #ifndef BRC_LIFE_BSTAT
 #define BRC_LIFE_BSTAT 0   // LANES, sender peers: the batch's step statistics by ballot popcounts instead of wave sums
 #endif
@@ -977,6 +980,31 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                 s_sv[lane] = m0 & 0xFFFFu;
                 if (wpg > 1) s_sv[64 + lane] = m1 & 0xFFFFu;
                 __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                if constexpr (BRC_LIFE_QBULK) {
+                    // a lane whose deliveries here (one origin: one host) can end no phase -- fewer than T_cnt -
+                    // vcount of them, or not in phase 1 / 2 -- and bring at most one value new to `order` takes
+                    // them at once: its host joins each value's set, vcount grows by their number (the
+                    // one-by-one loop below would do exactly this; only the insertion order of two or more new
+                    // values needs the phase order, so those go one by one)
+                    const uint32_t nb = (uint32_t)(__popcll(gb[0]) + __popcll(gb[1]));
+                    if (nb && ((phase != 1 && phase != 2) || vcount + nb < P.T_cnt)) {
+                        uint32_t V = 0;                       // values among the deliveries (bit v)
+                        for (uint32_t j = 0; j < wpg; ++j)
+                            for (uint64_t x = gb[j]; x; x &= x - 1)
+                                V |= 1u << (s_sv[j * 64 + (uint32_t)__builtin_ctzll(x)] >> 14);
+                        uint32_t known = 0;                   // values already in `order`
+                        for (uint32_t i = 0; i < nvals; ++i) known |= 1u << ((order >> (2 * i)) & 3u);
+                        const uint32_t nv = V & ~known;
+                        if ((nv & (nv - 1u)) == 0) {
+                            if (nv) { order |= ((uint32_t)__builtin_ctz(nv)) << (2 * nvals); ++nvals; }
+                            const uint64_t hb = 1ull << (w >> (ksh - 6));      // host = origin of the group
+                            for (uint32_t v = 0; v < 4; ++v)
+                                if ((V >> v) & 1u) s_hm[v * 64 + lane] |= hb;
+                            vcount += nb;
+                            gb[0] = gb[1] = 0;
+                        }
+                    }
+                }
                 while (gb[0] | gb[1]) {
                     uint32_t bs = 0xFFFFFFFFu, bk = 0;
                     for (uint32_t j = 0; j < wpg; ++j)

@@ -64,6 +64,9 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 #ifndef BRC_LIFE_QBULK
 #define BRC_LIFE_QBULK 1   // key windows of 64 / 128: a lane's deliveries of one origin at once when no phase can end
 #endif
+#ifndef BRC_LIFE_SKIP
+#define BRC_LIFE_SKIP 1   // LANES: a batch jumps to the next relative step some lane has pending
+#endif
 #ifndef BRC_LIFE_BSTAT
 #define BRC_LIFE_BSTAT 0   // LANES, sender peers: the batch's step statistics by ballot popcounts instead of wave sums
 #endif
@@ -668,8 +671,9 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
         uint32_t win[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) win[j] = 0;
+        uint32_t rstep = 1;                           // SKIP: steps to the next one some lane has pending
 #pragma unroll 1
-        for (uint32_t r = 1; ; ++r) {
+        for (uint32_t r = 1; ; r += rstep) {
             if (!__ballot(pend != 0u)) break;
             const bool hS = (pend & 1u) != 0, hE = (pend & (1u << 10)) != 0, hR = (pend & (1u << 20)) != 0;
             bool act = hS || hE || hR;
@@ -784,12 +788,32 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     if (nrA) pend |= 1u << 21;
                     if (vB) pend |= 1u << (20u + Dd);
                 }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) win[j] = win[j + 1];
-                win[8] = 0;
             }
             if (act) last = ts;
-            pend = (pend >> 1) & ~((1u << 9) | (1u << 19));   // step r consumed: the window moves to r + 1
+            if constexpr (BRC_LIFE_SKIP) {
+                // step r consumed; the window moves to the next step any lane of the batch has pending (the
+                // lowest offset over the three fields and the wave: no set bit crosses a field boundary)
+                pend &= ~(1u | (1u << 10) | (1u << 20));
+                uint32_t m = (pend | (pend >> 10) | (pend >> 20)) & 0x3FFu;
+                m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0xB1, 0xF, 0xF, true);
+                m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x4E, 0xF, 0xF, true);
+                m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x141, 0xF, 0xF, true);
+                m |= (uint32_t)__builtin_amdgcn_mov_dpp((int)m, 0x140, 0xF, 0xF, true);
+                m = uni32(rl(m, 0) | rl(m, 16) | rl(m, 32) | rl(m, 48));
+                rstep = m ? (uint32_t)__builtin_ctz(m) : 1u;
+                pend >>= rstep;
+            } else {
+                pend = (pend >> 1) & ~((1u << 9) | (1u << 19));   // step r consumed: the window moves to r + 1
+            }
+            if constexpr (CONN) {
+                // the READY-copy window moves with it (rstep <= 9 steps: entries past it are zero)
+#pragma unroll 1
+                for (uint32_t q = 0; q < rstep; ++q) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) win[j] = win[j + 1];
+                    win[8] = 0;
+                }
+            }
         }
         if (has) {
             mst(k, (mld(k) & 0xFFFFu) | (last << 16));

@@ -517,7 +517,10 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                             const uint64_t x = __ballot(c != 0);
                             if (x) {
                                 if (__ballot(c > 1u)) {
-                                    for (uint32_t b = 0; b < 8; ++b) {
+                                    // the count planes up to the wave's highest set bit (copies > 3 are rare)
+                                    uint32_t np = 2;
+                                    while (np < 8 && __ballot((c >> np) != 0u)) ++np;
+                                    for (uint32_t b = 0; b < np; ++b) {
                                         const uint64_t pb = __ballot((c >> b) & 1u);
                                         ra += (uint32_t)__popcll(pb & L[i]) << b;
                                     }

@@ -218,13 +218,21 @@ __global__ __launch_bounds__(NPAD, (EV ? BRC_MIN_WAVES_EV : WV ? WV : DM == 16 ?
     };
 
     // ---- outm[i][w]: senders with a delay-(i+1) link to some honest receiver; outset / dset
-#pragma unroll
-    for (int i = 0; i < DM; ++i) {
+    auto outm_row = [&](int i) {
         Unrolled<NW>::run([&](auto wc) {
             constexpr int w = decltype(wc)::value;
             const uint64_t x = wave_or64(honest ? Lw((uint32_t)i + 1, wc) : 0ull);
             if (lane == 0 && x) atomicOr((unsigned long long*)&s_outm[i * NW + w], (unsigned long long)x);
         });
+    };
+    if constexpr (DM > 8) {
+        // once-per-launch setup as a loop: unrolled, its 16 x NW wave reductions were most of the DM = 16
+        // instantiations' scratch instructions (504 -> 84 on cfg5 geometric, same kernel time)
+#pragma unroll 1
+        for (int i = 0; i < DM; ++i) outm_row(i);
+    } else {
+#pragma unroll
+        for (int i = 0; i < DM; ++i) outm_row(i);
     }
     __syncthreads();
     uint32_t outset = 0, dset = 0;

@@ -20,7 +20,8 @@ def main():
     print("%-58s %5s %6s %6s %8s %8s" % ("kernel", "vgpr", "vspill", "sspill", "scratchB", "scratchI"))
     for u in units:
         out = "/tmp/scratch_count.s"
-        subprocess.check_call(["hipcc"] + flags + ["--cuda-device-only", "-S", "-o", out, os.path.join(G.CSRC, u)],
+        subprocess.check_call(["hipcc"] + flags + G.UNIT_FLAGS.get(u, []) + ["--cuda-device-only", "-S", "-o", out,
+                                                                        os.path.join(G.CSRC, u)],
                               stderr=subprocess.DEVNULL)
         text = open(out).read()
         bodies = {}

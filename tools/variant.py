@@ -33,7 +33,8 @@ def main():
         obj = os.path.join(out, unit.replace(".hip", ".o"))
         objs.append(obj)
         mine.append(obj)
-        procs.append(subprocess.Popen(["hipcc"] + G.HIP_FLAGS_C + flags + ["-o", obj, os.path.join(G.CSRC, unit)],
+        procs.append(subprocess.Popen(["hipcc"] + G.HIP_FLAGS_C + G.UNIT_FLAGS.get(unit, []) + flags +
+                                      ["-o", obj, os.path.join(G.CSRC, unit)],
                                       cwd=ROOT))
     if any(p.wait() for p in procs):
         sys.exit("hipcc failed")

@@ -67,6 +67,9 @@ __device__ __forceinline__ uint32_t lm_tend(uint32_t m) { return m >> 16; }
 #ifndef BRC_LIFE_SKIP
 #define BRC_LIFE_SKIP 1   // LANES: a batch jumps to the next relative step some lane has pending
 #endif
+#ifndef BRC_LIFE_HSTAT
+#define BRC_LIFE_HSTAT 1   // LANES, sender peers: one wave sum per batch step, the 0/1 statistics by ballots
+#endif
 #ifndef BRC_LIFE_BSTAT
 #define BRC_LIFE_BSTAT 0   // LANES, sender peers: the batch's step statistics by ballot popcounts instead of wave sums
 #endif
@@ -740,6 +743,13 @@ __global__ __launch_bounds__(64, PL ? (MODE == KMODE_CONN ? BRC_LIFE_PL_CONN_WAV
                     const uint32_t sA = nHF * (pc(e1) + pc(q1)) + nHS * n2 + pc(saA != 0);
                     const uint32_t sB = nHF * (pc(e3) + pc(q3)) + nHS * n2 + pc(saB != 0);
                     arr = nHF * sA + nHS * sB;
+                    msgs = n * (nHF * (pc(esA != 0) + pc(rsA != 0)) + nHS * (pc(esB != 0) + pc(rsB != 0)));
+                    cells = nHF * pc(aA != 0) + nHS * pc(aB != 0);
+                } else if constexpr (BRC_LIFE_HSTAT) {
+                    // one wave sum (the arrival counts); the 0/1 terms as ballot popcounts
+                    auto pc = [&](bool c) -> uint32_t { return (uint32_t)__popcll(__ballot(c)); };
+                    const uint32_t s1 = wave_sum(aA | (aB << 16));
+                    arr = nHF * (s1 & 0xFFFFu) + nHS * (s1 >> 16);
                     msgs = n * (nHF * (pc(esA != 0) + pc(rsA != 0)) + nHS * (pc(esB != 0) + pc(rsB != 0)));
                     cells = nHF * pc(aA != 0) + nHS * pc(aB != 0);
                 } else {
